@@ -1,0 +1,152 @@
+/*
+ * ii.h — C ABI of the MI355X inverted-index builder (libii.so).
+ *
+ * Drop-in boundary for the reference's mapper/reducer path
+ * (/root/reference/main.c).  The reference has no library API: its path sits
+ * behind the CLI `tema1 <M> <R> <list>` (main.c:246-255) and the pthread
+ * entry points mapper()/reducer() (main.c:85, main.c:126) joined by the
+ * partial_<letter>.txt files (main.c:332-341).  Each entry point below names
+ * the reference code it replaces.  All signatures use plain C types and
+ * pointers only.
+ *
+ * Ownership: the caller owns the file list, paths and input buffers; the
+ * context owns every device and host buffer it allocates, including the
+ * text returned by ii_letter_text (valid until the next ii_map_* / ii_reduce
+ * call or ii_close).
+ * Errors: 0 = OK, negative = error code (ii_strerror).  Calls on one context
+ * are not re-entrant; use one context per GPU.
+ */
+#ifndef II_H
+#define II_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define II_ALPHABET 26 /* main.c:9 ALPHABET_SIZE */
+#define II_MAX_WORD 300 /* main.c:7 MAX_WORD: cleaned words keep <= 299 letters */
+
+enum {
+    II_OK = 0,
+    II_ERR_ARG = -1,        /* bad argument (NULL, out-of-range, unsorted IDs) */
+    II_ERR_HIP = -2,        /* a HIP runtime call failed */
+    II_ERR_NOMEM = -3,      /* device or host allocation failed */
+    II_ERR_IO = -4,         /* list file unreadable / malformed (main.c:257-285) */
+    II_ERR_STATE = -5,      /* call out of order (e.g. ii_reduce before any map) */
+    II_ERR_LAYOUT = -6,     /* device text violates the separator contract */
+    II_ERR_INTERNAL = -7,   /* internal consistency check failed */
+    II_ERR_NODEV = -8       /* no HIP device */
+};
+
+typedef struct ii_ctx ii_ctx;
+
+/* One input file of a shard.  Replaces FileInfo (main.c:14-18).  id0 is the
+ * 0-based position in the list file (main.c:275) and is printed as id0+1
+ * (main.c:116). */
+typedef struct {
+    const char *path;
+    uint64_t size;
+    uint32_t id0;
+} ii_file;
+
+/* Per-run counters (no reference equivalent; the reference only prints). */
+typedef struct {
+    uint64_t bytes;        /* input bytes indexed (B) */
+    uint64_t tokens;       /* kept tokens T (= lines the reference writes to partial files) */
+    uint64_t pairs;        /* unique (word, file) pairs U */
+    uint64_t words;        /* distinct words V */
+    uint64_t long_tokens;  /* tokens with more than 12 letters */
+    uint64_t out_bytes;    /* bytes of the 26 letter texts */
+    uint64_t table_cap;    /* word-table capacity (slots) */
+    uint32_t retries;      /* word-table regrows / rehashes in the last map */
+    uint32_t sort_passes;  /* radix passes of the token sort */
+    uint64_t letter_tokens[II_ALPHABET]; /* tokens per first letter (partial_<l>.txt line counts) */
+    /* device time per phase, milliseconds (hipEvent, stream-ordered) */
+    double ms_map;         /* tokenize + word table (K1) */
+    double ms_dict;        /* dictionary / lexicographic ids */
+    double ms_sort;        /* token sort (K2) */
+    double ms_reduce;      /* unique + postings (K3) */
+    double ms_order;       /* final order (K4) */
+    double ms_format;      /* text formatting (K5) */
+    double ms_total;
+    /* dominant kernel: the radix scatter of the token sort */
+    double scatter_ms_avg; /* average duration of one token-sort scatter launch */
+    uint64_t scatter_bytes;/* algorithmic bytes of one token-sort scatter launch */
+    uint32_t scatter_launches;
+} ii_stats;
+
+/* Open a context on HIP device `device`. */
+int ii_open(ii_ctx **out, int device);
+void ii_close(ii_ctx *ctx);
+const char *ii_strerror(int code);
+
+/*
+ * Map phase.  Replaces mapper() (main.c:85-124) for a whole shard plus the
+ * partial-file shuffle (main.c:332-341, 116, 371-373): tokens become
+ * device-resident (word, file) records; hist_out (may be NULL) receives the
+ * number of tokens per first letter, i.e. the line counts the reference
+ * would have written to partial_<letter>.txt.
+ *
+ * Files must be given in ascending id0 order.  Missing / unreadable files are
+ * reported on stderr in the reference's wording (main.c:98) and contribute
+ * nothing; they are not an error.  `nthreads` host reader threads (the
+ * reference's M) read the files.
+ */
+int ii_map_files(ii_ctx *ctx, const ii_file *files, uint32_t nfiles, int nthreads,
+                 uint64_t hist_out[II_ALPHABET]);
+
+/* Map phase over host memory: file f is text[file_off[f] .. file_off[f+1]),
+ * with IDs file_id0[f] (ascending). */
+int ii_map_host(ii_ctx *ctx, const uint8_t *text, const uint64_t *file_off, const uint32_t *file_id0,
+                uint32_t nfiles, uint64_t hist_out[II_ALPHABET]);
+
+/* Map phase over device-resident text (no host copy of the text).
+ * d_text holds nbytes bytes; host arrays file_start (nfiles entries) and
+ * file_id0 (ascending) describe the files: file f starts at file_start[f] and
+ * ends where the next begins (or at nbytes).  Separator contract: for every
+ * f > 0 with file_start[f] > 0, d_text[file_start[f] - 1] must be C-locale
+ * whitespace, so no token can span two files (checked: II_ERR_LAYOUT).
+ * d_text must be 16-byte aligned (II_ERR_ARG otherwise).
+ * The context keeps a pointer to d_text until the next map call. */
+int ii_map_device(ii_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uint64_t *file_start,
+                  const uint32_t *file_id0, uint32_t nfiles, uint64_t hist_out[II_ALPHABET]);
+
+/*
+ * Reduce phase.  Replaces reducer() (main.c:126-242) for all 26 letters:
+ * group by word, distinct file IDs (main.c:170-213), order by (df desc,
+ * word asc) with ascending IDs (main.c:55-64, 215-226), and format every
+ * line "word:[id id ...]\n" (main.c:227-234) — all on the device.
+ * With copy_text != 0 the text is also copied to host memory for
+ * ii_letter_text; with 0 it stays device-resident (benchmarking).
+ */
+int ii_reduce(ii_ctx *ctx, int copy_text);
+
+/* Text of <letter>.txt (letter 0..25 = 'a'..'z'), valid until the next call. */
+int ii_letter_text(ii_ctx *ctx, int letter, const char **buf, size_t *len);
+
+/* Counters and phase timings of the last map + reduce. */
+int ii_get_stats(ii_ctx *ctx, ii_stats *out);
+
+/* Device pointer + byte offsets of the formatted index (device-resident
+ * output, letter l = [letter_off[l], letter_off[l+1])). */
+int ii_device_text(ii_ctx *ctx, const uint8_t **d_text, uint64_t letter_off[II_ALPHABET + 1]);
+
+/* Reducer letter range (main.c:129-130): reducer r of R owns
+ * [(26/R)*r, r == R-1 ? 26 : (26/R)*(r+1)).  Pure host arithmetic. */
+int ii_reducer_letters(int r, int R, int *lo, int *hi);
+
+/* Size-sorted greedy shard partition (main.c:21-25, 300-323), defined for
+ * every M >= 1 (empty shards where the reference is undefined):
+ * order[] receives the file indices sorted by (size desc, index asc);
+ * shard_begin/shard_end (M entries each) receive [begin, end) ranges into
+ * order[].  Pure host arithmetic. */
+int ii_partition(const uint64_t *sizes, uint32_t nfiles, int M, uint32_t *order, uint32_t *shard_begin,
+                 uint32_t *shard_end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* II_H */

@@ -1,0 +1,305 @@
+/*
+ * ii_oracle.c — CPU restatement of the reference inverted-index semantics.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity CHECKER for the MI355X
+ * product path; it is never linked into, called by, or shipped with the
+ * product (libii.so / ii_index).  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may use it.
+ *
+ * Parity is PINNED: outputs of this restatement are checked byte-for-byte
+ * against outputs of the reference binary itself (oracle/_ref/tema1, built
+ * from /root/reference/main.c by oracle/Makefile) on every fixture under
+ * tests/golden/ (configs 1 and 2, the edge corpus, seeded random corpora).
+ *
+ * What it restates (reference = /root/reference/main.c):
+ *   - file list: count, then `count` whitespace-delimited names; ID = list
+ *     position (main.c:263-285, id at main.c:275, printed id+1 at main.c:116)
+ *   - tokenizer: fscanf("%s") whitespace tokens, C-locale isspace set
+ *     (main.c:102)
+ *   - cleaning: keep A-Z (+32) and a-z, stop at the first NUL, at most
+ *     MAX_WORD-1 = 299 letters, drop tokens with no letters (main.c:103-113)
+ *   - bucketing by first letter (main.c:114-116)
+ *   - reducer: distinct file IDs per word (main.c:170-213, add_number
+ *     main.c:67-77)
+ *   - order: df descending, then strcmp ascending (compare_word_entries
+ *     main.c:55-64, qsort main.c:215); IDs ascending (main.c:217-226)
+ *   - writer: "word:[id id ...]\n" into <letter>.txt (main.c:227-234)
+ * Reference UB is defined as SURVEY.md §9.11 says: raw tokens longer than 299
+ * bytes keep their first 299 letters; any number of files.
+ *
+ * The restatement groups with a hash map instead of the reference's linear
+ * scan (main.c:172-173) — same result, O(T) instead of O(T*V).
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#define OR_MAX_WORD 300 /* main.c:7 */
+#define OR_ALPHA 26     /* main.c:9 */
+
+/* C-locale isspace (fscanf %s delimiter set, main.c:102). */
+static inline int or_isspace(unsigned char c) {
+    return c == ' ' || (c >= 0x09 && c <= 0x0d);
+}
+
+typedef struct {
+    char *word;     /* cleaned word, NUL-terminated */
+    uint32_t len;
+    uint64_t hash;
+    uint32_t *ids;  /* distinct 1-based file IDs, ascending (files are visited in ID order) */
+    uint32_t n, cap;
+} or_entry;
+
+typedef struct {
+    or_entry *e;
+    uint32_t n, cap;     /* entries */
+    uint32_t *slot;      /* open-addressing table of entry index + 1 */
+    uint64_t mask;
+} or_dict;
+
+static uint64_t or_hash(const char *s, uint32_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t i = 0; i < n; i++) { h ^= (unsigned char)s[i]; h *= 1099511628211ull; }
+    return h ^ (h >> 29);
+}
+
+static void or_dict_grow(or_dict *d) {
+    uint64_t ncap = d->mask ? (d->mask + 1) * 2 : 1024;
+    uint32_t *ns = calloc(ncap, sizeof(uint32_t));
+    if (!ns) { fprintf(stderr, "oracle: out of memory\n"); exit(EXIT_FAILURE); }
+    for (uint32_t i = 0; i < d->n; i++) {
+        uint64_t s = d->e[i].hash & (ncap - 1);
+        while (ns[s]) s = (s + 1) & (ncap - 1);
+        ns[s] = i + 1;
+    }
+    free(d->slot);
+    d->slot = ns;
+    d->mask = ncap - 1;
+}
+
+/* Record (word, id1) — the reducer's "find word, add id if new" step
+ * (main.c:170-213).  Because files are visited in ascending ID order, a
+ * duplicate ID is always the last one appended. */
+static void or_dict_add(or_dict *d, const char *w, uint32_t n, uint32_t id1) {
+    if ((uint64_t)(d->n + 1) * 2 > d->mask + 1) or_dict_grow(d);
+    uint64_t h = or_hash(w, n);
+    uint64_t s = h & d->mask;
+    for (;;) {
+        uint32_t x = d->slot[s];
+        if (!x) break;
+        or_entry *e = &d->e[x - 1];
+        if (e->hash == h && e->len == n && memcmp(e->word, w, n) == 0) {
+            if (e->ids[e->n - 1] != id1) {
+                if (e->n == e->cap) {
+                    e->cap *= 2;
+                    e->ids = realloc(e->ids, e->cap * sizeof(uint32_t));
+                    if (!e->ids) { fprintf(stderr, "oracle: out of memory\n"); exit(EXIT_FAILURE); }
+                }
+                e->ids[e->n++] = id1;
+            }
+            return;
+        }
+        s = (s + 1) & d->mask;
+    }
+    if (d->n == d->cap) {
+        d->cap = d->cap ? d->cap * 2 : 1024;
+        d->e = realloc(d->e, d->cap * sizeof(or_entry));
+        if (!d->e) { fprintf(stderr, "oracle: out of memory\n"); exit(EXIT_FAILURE); }
+    }
+    or_entry *e = &d->e[d->n];
+    e->word = malloc(n + 1);
+    memcpy(e->word, w, n);
+    e->word[n] = 0;
+    e->len = n;
+    e->hash = h;
+    e->cap = 4;
+    e->ids = malloc(e->cap * sizeof(uint32_t));
+    e->ids[0] = id1;
+    e->n = 1;
+    d->slot[s] = ++d->n;
+}
+
+/* Tokenize one file's bytes (mapper hot loop, main.c:102-118). */
+static void or_map_bytes(or_dict dicts[OR_ALPHA], const unsigned char *p, uint64_t len, uint32_t id1) {
+    char clean[OR_MAX_WORD];
+    uint64_t i = 0;
+    while (i < len) {
+        while (i < len && or_isspace(p[i])) i++;
+        if (i >= len) break;
+        /* token = maximal run of non-space bytes (NUL is not a delimiter) */
+        uint32_t j = 0;
+        int stopped = 0; /* cleaning loop ended: NUL seen or 299 letters (main.c:105) */
+        while (i < len && !or_isspace(p[i])) {
+            unsigned char c = p[i++];
+            if (stopped) continue;
+            if (c == 0) { stopped = 1; continue; }
+            if (c >= 'A' && c <= 'Z') clean[j++] = (char)(c + 32);
+            else if (c >= 'a' && c <= 'z') clean[j++] = (char)c;
+            if (j >= OR_MAX_WORD - 1) stopped = 1;
+        }
+        if (j > 0) or_dict_add(&dicts[clean[0] - 'a'], clean, j, id1);
+    }
+}
+
+static int or_cmp(const void *a, const void *b) {
+    const or_entry *x = a, *y = b;
+    if (x->n != y->n) return x->n > y->n ? -1 : 1; /* df descending, main.c:59-61 */
+    return strcmp(x->word, y->word);                /* word ascending, main.c:63 */
+}
+
+static uint32_t or_digits(uint32_t v) {
+    uint32_t d = 1;
+    while (v >= 10) { v /= 10; d++; }
+    return d;
+}
+
+/* Format one letter's entries (writer, main.c:227-234). Returns malloc'd text. */
+static char *or_reduce_letter(or_dict *d, uint64_t *out_len) {
+    qsort(d->e, d->n, sizeof(or_entry), or_cmp);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+        total += d->e[i].len + 4; /* ":[" "]\n" */
+        for (uint32_t k = 0; k < d->e[i].n; k++) total += or_digits(d->e[i].ids[k]) + (k ? 1 : 0);
+    }
+    char *buf = malloc(total + 1);
+    char *o = buf;
+    for (uint32_t i = 0; i < d->n; i++) {
+        or_entry *e = &d->e[i];
+        memcpy(o, e->word, e->len); o += e->len;
+        *o++ = ':'; *o++ = '[';
+        for (uint32_t k = 0; k < e->n; k++) {
+            if (k) *o++ = ' ';
+            o += sprintf(o, "%u", e->ids[k]);
+        }
+        *o++ = ']'; *o++ = '\n';
+    }
+    *out_len = (uint64_t)(o - buf);
+    return buf;
+}
+
+static void or_dict_free(or_dict *d) {
+    for (uint32_t i = 0; i < d->n; i++) { free(d->e[i].word); free(d->e[i].ids); }
+    free(d->e); free(d->slot);
+    memset(d, 0, sizeof(*d));
+}
+
+/*
+ * In-memory entry point (used by tests and bench.py's cpu_baseline):
+ *   text      concatenated file bytes
+ *   file_off  nfiles+1 offsets into text; file f = [file_off[f], file_off[f+1])
+ *   file_id0  0-based file IDs (printed as id0+1); must be ascending
+ *   out       receives a malloc'd buffer holding the 26 letter texts back to back
+ *   letter_off receives 27 offsets into *out
+ * Returns 0.  Free *out with ii_oracle_free.
+ */
+int ii_oracle_index(const unsigned char *text, const uint64_t *file_off, const uint32_t *file_id0,
+                    uint32_t nfiles, char **out, uint64_t letter_off[OR_ALPHA + 1]) {
+    for (uint32_t f = 1; f < nfiles; f++)
+        if (file_id0[f] <= file_id0[f - 1]) return -1; /* IDs must ascend */
+    or_dict dicts[OR_ALPHA];
+    memset(dicts, 0, sizeof(dicts));
+    for (uint32_t f = 0; f < nfiles; f++)
+        or_map_bytes(dicts, text + file_off[f], file_off[f + 1] - file_off[f], file_id0[f] + 1);
+    char *parts[OR_ALPHA];
+    uint64_t lens[OR_ALPHA], total = 0;
+    for (int l = 0; l < OR_ALPHA; l++) {
+        parts[l] = or_reduce_letter(&dicts[l], &lens[l]);
+        total += lens[l];
+        or_dict_free(&dicts[l]);
+    }
+    char *buf = malloc(total + 1);
+    uint64_t o = 0;
+    for (int l = 0; l < OR_ALPHA; l++) {
+        letter_off[l] = o;
+        memcpy(buf + o, parts[l], lens[l]);
+        o += lens[l];
+        free(parts[l]);
+    }
+    letter_off[OR_ALPHA] = o;
+    *out = buf;
+    return 0;
+}
+
+void ii_oracle_free(void *p) { free(p); }
+
+#ifdef II_ORACLE_MAIN
+/* Same CLI as the reference: <num_mappers> <num_reducers> <input_file_list>
+ * (main.c:246-260); outputs a.txt..z.txt in the CWD. */
+static unsigned char *or_read_file(const char *path, uint64_t *len) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    uint64_t cap = 1 << 16, n = 0;
+    unsigned char *b = malloc(cap);
+    size_t r;
+    while ((r = fread(b + n, 1, cap - n, f)) > 0) {
+        n += r;
+        if (n == cap) { cap *= 2; b = realloc(b, cap); }
+    }
+    fclose(f);
+    *len = n;
+    return b;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) {
+        fprintf(stderr, "Usage: %s <num_mappers> <num_reducers> <input_file_list>\n", argv[0]);
+        return -1;
+    }
+    int num_reducers = atoi(argv[2]);
+    FILE *fl = fopen(argv[3], "r");
+    if (!fl) { fprintf(stderr, "Error opening input file list: %s\n", argv[3]); return -1; }
+    int count;
+    if (fscanf(fl, "%d", &count) != 1) {
+        fprintf(stderr, "Error reading the number of files from input file list\n");
+        fclose(fl);
+        return -1;
+    }
+    if (count < 0) count = 0;
+    char **names = calloc((size_t)count + 1, sizeof(char *));
+    for (int i = 0; i < count; i++) {
+        names[i] = malloc(4096);
+        if (fscanf(fl, "%4095s", names[i]) != 1) {
+            fprintf(stderr, "Error reading file name from input file list\n");
+            fclose(fl);
+            return -1;
+        }
+    }
+    fclose(fl);
+    unsigned char *text = NULL;
+    uint64_t tlen = 0, tcap = 0;
+    uint64_t *off = malloc(((size_t)count + 1) * sizeof(uint64_t));
+    uint32_t *ids = malloc(((size_t)count + 1) * sizeof(uint32_t));
+    for (int i = 0; i < count; i++) {
+        struct stat st;
+        if (stat(names[i], &st) != 0) fprintf(stderr, "Error getting size of file: %s\n", names[i]);
+        off[i] = tlen;
+        ids[i] = (uint32_t)i;
+        uint64_t n = 0;
+        unsigned char *b = or_read_file(names[i], &n);
+        if (!b) { fprintf(stderr, "Mapper %d: Error opening file %s\n", 0, names[i]); continue; }
+        if (tlen + n > tcap) { tcap = (tlen + n) * 2 + 1024; text = realloc(text, tcap); }
+        memcpy(text + tlen, b, n);
+        tlen += n;
+        free(b);
+    }
+    off[count] = tlen;
+    char *out;
+    uint64_t loff[OR_ALPHA + 1];
+    ii_oracle_index(text ? text : (unsigned char *)"", off, ids, (uint32_t)count, &out, loff);
+    if (num_reducers > 0) {
+        for (int l = 0; l < OR_ALPHA; l++) {
+            char fn[16];
+            snprintf(fn, sizeof(fn), "%c.txt", 'a' + l);
+            FILE *o = fopen(fn, "w");
+            if (!o) { fprintf(stderr, "Error creating output file: %s\n", fn); return -1; }
+            fwrite(out + loff[l], 1, loff[l + 1] - loff[l], o);
+            fclose(o);
+        }
+    }
+    free(out);
+    return 0;
+}
+#endif

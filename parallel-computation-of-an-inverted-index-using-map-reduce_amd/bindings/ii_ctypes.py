@@ -1,0 +1,215 @@
+"""ctypes binding of libii.so (include/ii.h) and libiigen.so.
+
+This is the Python-side caller of the C ABI — the same binding a maintainer
+of the reference would add to drive the MI355X path from a script (see
+INTEGRATION.md).  It loads the in-tree libraries and raises if they are
+missing: there is no CPU fallback.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ALPHABET = 26
+
+II_OK = 0
+ERRORS = {
+    -1: "II_ERR_ARG", -2: "II_ERR_HIP", -3: "II_ERR_NOMEM", -4: "II_ERR_IO", -5: "II_ERR_STATE",
+    -6: "II_ERR_LAYOUT", -7: "II_ERR_INTERNAL", -8: "II_ERR_NODEV",
+}
+
+
+class IIError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s failed: %s (%d)" % (what, ERRORS.get(code, "?"), code))
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("bytes", ctypes.c_uint64), ("tokens", ctypes.c_uint64), ("pairs", ctypes.c_uint64),
+        ("words", ctypes.c_uint64), ("long_tokens", ctypes.c_uint64), ("out_bytes", ctypes.c_uint64),
+        ("table_cap", ctypes.c_uint64), ("retries", ctypes.c_uint32), ("sort_passes", ctypes.c_uint32),
+        ("letter_tokens", ctypes.c_uint64 * ALPHABET),
+        ("ms_map", ctypes.c_double), ("ms_dict", ctypes.c_double), ("ms_sort", ctypes.c_double),
+        ("ms_reduce", ctypes.c_double), ("ms_order", ctypes.c_double), ("ms_format", ctypes.c_double),
+        ("ms_total", ctypes.c_double), ("scatter_ms_avg", ctypes.c_double), ("scatter_bytes", ctypes.c_uint64),
+        ("scatter_launches", ctypes.c_uint32),
+    ]
+
+    def as_dict(self):
+        d = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            d[name] = list(v) if name == "letter_tokens" else v
+        return d
+
+
+class IIFile(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("size", ctypes.c_uint64), ("id0", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(PKG_DIR, "libii.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError("libii.so not built (make -C %s)" % PKG_DIR)
+        L = ctypes.CDLL(path)
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.ii_open.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
+        L.ii_close.argtypes = [ctypes.c_void_p]
+        L.ii_close.restype = None
+        L.ii_strerror.argtypes = [ctypes.c_int]
+        L.ii_strerror.restype = ctypes.c_char_p
+        L.ii_map_files.argtypes = [ctypes.c_void_p, ctypes.POINTER(IIFile), ctypes.c_uint32, ctypes.c_int, u64p]
+        L.ii_map_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u64p, u32p, ctypes.c_uint32, u64p]
+        L.ii_map_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, u64p, u32p, ctypes.c_uint32,
+                                    u64p]
+        L.ii_reduce.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.ii_letter_text.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                     ctypes.POINTER(ctypes.c_size_t)]
+        L.ii_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.ii_device_text.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), u64p]
+        L.ii_reducer_letters.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_int)]
+        L.ii_partition.argtypes = [u64p, ctypes.c_uint32, ctypes.c_int, u32p, u32p, u32p]
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != II_OK:
+        raise IIError(rc, what)
+
+
+def _u64(seq):
+    return (ctypes.c_uint64 * max(1, len(seq)))(*seq)
+
+
+def _u32(seq):
+    return (ctypes.c_uint32 * max(1, len(seq)))(*seq)
+
+
+class Index:
+    """One context on one GPU (ii_open .. ii_close)."""
+
+    def __init__(self, device=0):
+        self.h = ctypes.c_void_p()
+        _check(lib().ii_open(ctypes.byref(self.h), device), "ii_open")
+
+    def close(self):
+        if self.h:
+            lib().ii_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def map_host(self, text, file_off, file_id0):
+        """text: bytes/bytearray/numpy u8; file f = text[file_off[f]:file_off[f+1]]."""
+        n = len(file_id0)
+        hist = (ctypes.c_uint64 * ALPHABET)()
+        if hasattr(text, "ctypes"):
+            ptr = text.ctypes.data
+        else:
+            buf = (ctypes.c_uint8 * max(1, len(text))).from_buffer_copy(bytes(text) or b"\0")
+            ptr = ctypes.addressof(buf)
+        _check(lib().ii_map_host(self.h, ptr, _u64(file_off), _u32(file_id0), n, hist), "ii_map_host")
+        return list(hist)
+
+    def map_device(self, d_text_ptr, nbytes, file_start, file_id0):
+        hist = (ctypes.c_uint64 * ALPHABET)()
+        _check(lib().ii_map_device(self.h, ctypes.c_void_p(d_text_ptr), nbytes, _u64(file_start), _u32(file_id0),
+                                   len(file_id0), hist), "ii_map_device")
+        return list(hist)
+
+    def map_files(self, paths, nthreads=4, id0=None):
+        files = (IIFile * max(1, len(paths)))()
+        keep = []
+        for i, p in enumerate(paths):
+            b = os.fsencode(p)
+            keep.append(b)
+            size = os.path.getsize(p) if os.path.exists(p) else 0
+            files[i] = IIFile(b, size, i if id0 is None else id0[i])
+        hist = (ctypes.c_uint64 * ALPHABET)()
+        _check(lib().ii_map_files(self.h, files, len(paths), nthreads, hist), "ii_map_files")
+        return list(hist)
+
+    def reduce(self, copy_text=True):
+        _check(lib().ii_reduce(self.h, 1 if copy_text else 0), "ii_reduce")
+
+    def letter_text(self, letter):
+        buf = ctypes.c_char_p()
+        n = ctypes.c_size_t()
+        _check(lib().ii_letter_text(self.h, letter, ctypes.byref(buf), ctypes.byref(n)), "ii_letter_text")
+        return ctypes.string_at(buf, n.value) if n.value else b""
+
+    def letters(self):
+        return {chr(97 + l): self.letter_text(l) for l in range(ALPHABET)}
+
+    def stats(self):
+        s = Stats()
+        _check(lib().ii_get_stats(self.h, ctypes.byref(s)), "ii_get_stats")
+        return s
+
+    def device_text(self):
+        p = ctypes.c_void_p()
+        off = (ctypes.c_uint64 * (ALPHABET + 1))()
+        _check(lib().ii_device_text(self.h, ctypes.byref(p), off), "ii_device_text")
+        return p.value, list(off)
+
+
+def reducer_letters(r, R):
+    lo, hi = ctypes.c_int(), ctypes.c_int()
+    _check(lib().ii_reducer_letters(r, R, ctypes.byref(lo), ctypes.byref(hi)), "ii_reducer_letters")
+    return lo.value, hi.value
+
+
+def partition(sizes, M):
+    n = len(sizes)
+    order = (ctypes.c_uint32 * max(1, n))()
+    sb = (ctypes.c_uint32 * M)()
+    se = (ctypes.c_uint32 * M)()
+    _check(lib().ii_partition(_u64(sizes), n, M, order, sb, se), "ii_partition")
+    return list(order)[:n], list(sb), list(se)
+
+
+# ---------------------------------------------------------------- generator
+class GenParams(ctypes.Structure):
+    _fields_ = [("total_bytes", ctypes.c_uint64), ("nfiles", ctypes.c_uint32), ("vocab", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("size_sigma", ctypes.c_double)]
+
+
+_gen = None
+
+
+def genlib():
+    global _gen
+    if _gen is None:
+        path = os.path.join(PKG_DIR, "libiigen.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError("libiigen.so not built (make -C %s)" % PKG_DIR)
+        _gen = ctypes.CDLL(path)
+    return _gen
+
+
+def zipf_corpus(total_bytes, nfiles, vocab, seed, threads=8, out=None):
+    """Returns (numpy u8 text, numpy u64 file offsets[nfiles+1])."""
+    import numpy as np
+    p = GenParams(total_bytes, nfiles, vocab, seed, 1.0)
+    off = np.zeros(nfiles + 1, dtype=np.uint64)
+    if out is None:
+        out = np.empty(total_bytes + 16, dtype=np.uint8)
+    g = genlib()
+    if g.iigen_layout(ctypes.byref(p), ctypes.c_void_p(off.ctypes.data)) != 0:
+        raise RuntimeError("iigen_layout failed")
+    if g.iigen_fill(ctypes.byref(p), ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(out.ctypes.data), threads) != 0:
+        raise RuntimeError("iigen_fill failed")
+    return out[:total_bytes], off

@@ -1,0 +1,711 @@
+// ii_api.hip — C ABI (include/ii.h) and host orchestration of the MI355X
+// inverted-index pipeline.  One context = one GPU = one HIP stream; every
+// buffer is device-resident and reused across calls (grown on demand, never
+// freed inside the pipeline), sized for HBM3E rather than for a CPU page cache.
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/ii.h"
+#include "ii_kernels.h"
+
+using namespace ii;
+
+namespace {
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+constexpr int kMaxTimedPasses = 16;
+
+}  // namespace
+
+struct ii_ctx {
+    int dev = 0;
+    hipStream_t st = nullptr;
+
+    // input
+    DBuf text_own;  // text copied in by ii_map_host / ii_map_files
+    const uint8_t* text = nullptr;
+    uint64_t nbytes = 0;
+    uint32_t nfiles = 0;
+    uint32_t nfiles_total_hint = 0;  // upper bound of df when shards are merged
+    DBuf fstart, fid;
+
+    // scratch
+    DBuf partial, totals, counters, chunk_cnt, rtable;
+    // K1
+    DBuf rec, rec2, longs;
+    DBuf tkeys, trep;
+    uint64_t table_cap = 1ull << 22;
+    uint64_t long_cap = 0;
+    uint64_t seed = 0x51ed270b27a3f3c1ull;
+    // dictionary
+    DBuf dslot, dkey, dkey2, didx, didx2, remap, lkey, lrep, llen, lstart;
+    DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
+    // reduce / order / format
+    DBuf uniq, pstart, okey, okey2, oval, oval2, P, loff, out, letter_off;
+
+    uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
+    uint32_t retries = 0;
+    bool mapped = false, reduced = false;
+    uint64_t* rec_sorted = nullptr;
+    uint32_t* ord = nullptr;
+    uint64_t hist[II_ALPHABET] = {0};
+    uint64_t h_letter_off[II_ALPHABET + 1] = {0};
+    std::vector<char> host_text;
+    bool host_valid = false;
+
+    hipEvent_t ev[8] = {};
+    hipEvent_t ev_sc[2 * kMaxTimedPasses] = {};
+    int n_sc = 0;
+    ii_stats stats;
+};
+
+#define HIPCK(x)                                                                               \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "libii: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                                 \
+            return II_ERR_HIP;                                                                 \
+        }                                                                                      \
+    } while (0)
+
+#define CK(x)                   \
+    do {                        \
+        int r_ = (x);           \
+        if (r_ != II_OK) return r_; \
+    } while (0)
+
+static int grow(DBuf& b, size_t bytes) {
+    if (bytes <= b.cap && b.p) return II_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 8, 256);
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipMalloc(&b.p, std::max<size_t>(bytes, 256)) != hipSuccess) {
+            (void)hipGetLastError();
+            b.p = nullptr;
+            return II_ERR_NOMEM;
+        }
+        want = std::max<size_t>(bytes, 256);
+    }
+    b.cap = want;
+    return II_OK;
+}
+
+template <class T>
+static T* P_(DBuf& b) {
+    return reinterpret_cast<T*>(b.p);
+}
+
+static inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kBlock - 1) / kBlock); }
+static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
+
+// ----------------------------------------------------------------- scan / sort
+template <class Op>
+static int run_scan(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
+    if (n == 0) {
+        if (d_total) HIPCK(hipMemsetAsync(d_total, 0, sizeof(uint64_t), c->st));
+        return II_OK;
+    }
+    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kBlock - 1) / kBlock);
+    uint64_t chunk = ((n + nch - 1) / nch + kBlock - 1) / kBlock * kBlock;
+    nch = (n + chunk - 1) / chunk;
+    uint64_t* part = P_<uint64_t>(c->partial);
+    k_scan_reduce<Op><<<(uint32_t)nch, kBlock, 0, c->st>>>(op, n, chunk, part);
+    k_scan_partials<<<1, kBlock, 0, c->st>>>(part, (uint32_t)nch, d_total);
+    k_scan_apply<Op><<<(uint32_t)nch, kBlock, 0, c->st>>>(op, n, chunk, part);
+    HIPCK(hipGetLastError());
+    return II_OK;
+}
+
+struct OpInPlace {
+    uint64_t* a;
+    __device__ uint64_t value(uint64_t i) const { return a[i]; }
+    __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { a[i] = ex; }
+};
+
+// Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
+// [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
+static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
+                    bool timed, int* passes) {
+    if (passes) *passes = 0;
+    if (n <= 1 || hi <= lo) return II_OK;
+    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
+    uint64_t chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
+    nch = (n + chunk - 1) / chunk;
+    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * nch));
+    uint64_t* table = P_<uint64_t>(c->rtable);
+    const bool kv = v != nullptr;
+    for (int shift = lo; shift < hi; shift += kRadixBits) {
+        k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table);
+        CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
+        const bool ev = timed && c->n_sc < kMaxTimedPasses;
+        if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
+        if (kv)
+            k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift, (uint32_t)nch, table);
+        else
+            k_radix_scatter<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
+                                                                        (uint32_t)nch, table);
+        if (ev) {
+            HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
+            c->n_sc++;
+        }
+        HIPCK(hipGetLastError());
+        std::swap(*k, *k2);
+        if (kv) std::swap(*v, *v2);
+        if (passes) (*passes)++;
+    }
+    return II_OK;
+}
+
+static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
+    HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    HIPCK(hipStreamSynchronize(c->st));
+    return II_OK;
+}
+
+// ----------------------------------------------------------------- lifecycle
+extern "C" int ii_open(ii_ctx** out, int device) {
+    if (!out) return II_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return II_ERR_NODEV;
+    }
+    if (device < 0 || device >= n) return II_ERR_ARG;
+    ii_ctx* c = new ii_ctx();
+    c->dev = device;
+    HIPCK(hipSetDevice(device));
+    HIPCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
+    for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
+    if (grow(c->partial, sizeof(uint64_t) * (kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
+        grow(c->counters, sizeof(uint64_t) * C_NUM)) {
+        ii_close(c);
+        return II_ERR_NOMEM;
+    }
+    const char* s = getenv("II_TABLE_LOG2");
+    if (s && atoi(s) >= 10 && atoi(s) <= 34) c->table_cap = 1ull << atoi(s);
+    memset(&c->stats, 0, sizeof(c->stats));
+    *out = c;
+    return II_OK;
+}
+
+extern "C" void ii_close(ii_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->dev);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    DBuf* all[] = {&c->text_own, &c->fstart, &c->fid,   &c->partial, &c->totals, &c->counters, &c->chunk_cnt,
+                   &c->rtable,   &c->rec,    &c->rec2,  &c->longs,   &c->tkeys,  &c->trep,     &c->dslot,
+                   &c->dkey,     &c->dkey2,  &c->didx,  &c->didx2,   &c->remap,  &c->lkey,     &c->lrep,
+                   &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
+                   &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
+                   &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off};
+    for (DBuf* b : all)
+        if (b->p) (void)hipFree(b->p);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_sc)
+        if (e) (void)hipEventDestroy(e);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+}
+
+extern "C" const char* ii_strerror(int code) {
+    switch (code) {
+        case II_OK: return "ok";
+        case II_ERR_ARG: return "invalid argument";
+        case II_ERR_HIP: return "HIP runtime error";
+        case II_ERR_NOMEM: return "out of memory";
+        case II_ERR_IO: return "I/O error";
+        case II_ERR_STATE: return "call out of order";
+        case II_ERR_LAYOUT: return "device text violates the file separator contract";
+        case II_ERR_INTERNAL: return "internal consistency check failed";
+        case II_ERR_NODEV: return "no HIP device";
+        default: return "unknown error";
+    }
+}
+
+// ----------------------------------------------------------------- map (K1)
+static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
+    c->mapped = c->reduced = false;
+    c->host_valid = false;
+    c->n_sc = 0;
+    c->retries = 0;
+    memset(&c->stats, 0, sizeof(c->stats));
+    uint64_t* counters = P_<uint64_t>(c->counters);
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    HIPCK(hipEventRecord(c->ev[0], c->st));
+    HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
+    c->T = c->V = c->U = c->nlong = 0;
+    if (c->nbytes == 0 || c->nfiles == 0) {
+        memset(c->hist, 0, sizeof(c->hist));
+        if (hist_out) memset(hist_out, 0, sizeof(uint64_t) * II_ALPHABET);
+        HIPCK(hipEventRecord(c->ev[1], c->st));
+        HIPCK(hipEventRecord(c->ev[2], c->st));
+        c->mapped = true;
+        return II_OK;
+    }
+    const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
+    CK(grow(c->chunk_cnt, sizeof(uint64_t) * nch));
+    uint64_t* chunk_cnt = P_<uint64_t>(c->chunk_cnt);
+    const uint64_t* fstart = P_<uint64_t>(c->fstart);
+    const uint32_t* fid = P_<uint32_t>(c->fid);
+
+    k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, counters);
+    Table dummy{nullptr, nullptr, 0, 0, counters};
+    k_tokenize<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, dummy,
+                                                          nullptr, nullptr, 0);
+    CK(run_scan(c, OpInPlace{chunk_cnt}, nch, totals));
+    uint64_t hv[2];
+    CK(read_u64(c, totals, &hv[0]));
+    CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
+    if (hv[1] & 4) return II_ERR_LAYOUT;
+    c->T = hv[0];
+    CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+    CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+    if (c->long_cap < std::max<uint64_t>(1 << 16, c->T / 64)) c->long_cap = std::max<uint64_t>(1 << 16, c->T / 64);
+
+    for (int attempt = 0;; attempt++) {
+        if (attempt > 12) return II_ERR_INTERNAL;
+        CK(grow(c->tkeys, sizeof(uint64_t) * c->table_cap));
+        CK(grow(c->trep, sizeof(uint64_t) * c->table_cap));
+        CK(grow(c->longs, sizeof(LongTok) * c->long_cap));
+        HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * c->table_cap, c->st));
+        HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
+        Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->table_cap - 1, c->seed, counters};
+        k_tokenize<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
+                                                             P_<uint64_t>(c->rec), P_<LongTok>(c->longs), c->long_cap);
+        HIPCK(hipGetLastError());
+        uint64_t cnt[4];
+        CK(read_u64(c, counters, cnt, 4));
+        if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] * 2 > c->table_cap) {
+            c->table_cap *= 4;
+            c->retries++;
+            continue;
+        }
+        if (cnt[C_OVERFLOW] & 2) {
+            c->long_cap = cnt[C_LONG] + cnt[C_LONG] / 4 + 1024;
+            c->retries++;
+            continue;
+        }
+        c->nlong = cnt[C_LONG];
+        if (c->nlong) {
+            uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(c->nlong));
+            k_long_tokens<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong, tab,
+                                                 P_<uint64_t>(c->rec));
+            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong, P_<uint64_t>(c->rec),
+                                                 P_<uint64_t>(c->trep), counters);
+            HIPCK(hipGetLastError());
+            CK(read_u64(c, counters, cnt, 4));
+            if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] * 2 > c->table_cap) {
+                c->table_cap *= 4;
+                c->retries++;
+                continue;
+            }
+            if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
+                c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
+                c->retries++;
+                continue;
+            }
+        }
+        c->V = cnt[C_INSERT];
+        break;
+    }
+    CK(read_u64(c, counters + C_HIST, c->hist, II_ALPHABET));
+    if (hist_out) memcpy(hist_out, c->hist, sizeof(c->hist));
+    HIPCK(hipEventRecord(c->ev[1], c->st));
+    c->mapped = true;
+    return II_OK;
+}
+
+static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file_id0, uint32_t nfiles) {
+    for (uint32_t f = 1; f < nfiles; f++)
+        if (file_id0[f] <= file_id0[f - 1] || file_start[f] < file_start[f - 1]) return II_ERR_ARG;
+    if (nfiles && file_start[nfiles - 1] > c->nbytes) return II_ERR_ARG;
+    CK(grow(c->fstart, sizeof(uint64_t) * (nfiles + 1)));
+    CK(grow(c->fid, sizeof(uint32_t) * (nfiles + 1)));
+    if (nfiles) {
+        HIPCK(hipMemcpyAsync(c->fstart.p, file_start, sizeof(uint64_t) * nfiles, hipMemcpyHostToDevice, c->st));
+        HIPCK(hipMemcpyAsync(c->fid.p, file_id0, sizeof(uint32_t) * nfiles, hipMemcpyHostToDevice, c->st));
+        HIPCK(hipStreamSynchronize(c->st));  // caller's host arrays may go away after return
+    }
+    c->nfiles = nfiles;
+    return II_OK;
+}
+
+extern "C" int ii_map_device(ii_ctx* c, const uint8_t* d_text, uint64_t nbytes, const uint64_t* file_start,
+                             const uint32_t* file_id0, uint32_t nfiles, uint64_t hist_out[II_ALPHABET]) {
+    if (!c || (nfiles && (!file_start || !file_id0)) || (nbytes && !d_text)) return II_ERR_ARG;
+    if (((uintptr_t)d_text & 15u) != 0) return II_ERR_ARG;  // 16-byte staging loads
+    HIPCK(hipSetDevice(c->dev));
+    c->text = d_text;
+    c->nbytes = nbytes;
+    CK(set_files(c, file_start, file_id0, nfiles));
+    return map_core(c, hist_out);
+}
+
+static bool host_ws(uint8_t ch) { return ch == ' ' || (ch >= 9 && ch <= 13); }
+
+// Lay files out back to back, inserting '\n' after a file whose last byte is
+// not whitespace (separator contract), then one H2D copy.
+extern "C" int ii_map_host(ii_ctx* c, const uint8_t* text, const uint64_t* file_off, const uint32_t* file_id0,
+                           uint32_t nfiles, uint64_t hist_out[II_ALPHABET]) {
+    if (!c || (nfiles && (!file_off || !file_id0 || !text))) return II_ERR_ARG;
+    HIPCK(hipSetDevice(c->dev));
+    for (uint32_t f = 0; f < nfiles; f++)
+        if (file_off[f + 1] < file_off[f]) return II_ERR_ARG;
+    uint64_t total = nfiles ? file_off[nfiles] - file_off[0] + nfiles : 0;
+    std::vector<uint8_t> stage(total + 1);
+    std::vector<uint64_t> fs(nfiles);
+    uint64_t o = 0;
+    for (uint32_t f = 0; f < nfiles; f++) {
+        fs[f] = o;
+        uint64_t n = file_off[f + 1] - file_off[f];
+        if (n) memcpy(stage.data() + o, text + file_off[f], n);
+        o += n;
+        if (f + 1 < nfiles && (n == 0 || !host_ws(stage[o - 1]))) stage[o++] = '\n';
+    }
+    CK(grow(c->text_own, std::max<uint64_t>(o, 16)));
+    if (o) HIPCK(hipMemcpyAsync(c->text_own.p, stage.data(), o, hipMemcpyHostToDevice, c->st));
+    HIPCK(hipStreamSynchronize(c->st));
+    c->text = P_<uint8_t>(c->text_own);
+    c->nbytes = o;
+    CK(set_files(c, fs.data(), file_id0, nfiles));
+    return map_core(c, hist_out);
+}
+
+namespace {
+struct ReadJob {
+    const ii_file* files;
+    uint32_t n;
+    std::vector<std::vector<uint8_t>>* data;
+    uint32_t next;
+    pthread_mutex_t mu;
+};
+void* read_worker(void* arg) {
+    ReadJob* j = (ReadJob*)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        uint32_t f = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (f >= j->n) break;
+        FILE* fp = fopen(j->files[f].path, "rb");
+        if (!fp) {
+            fprintf(stderr, "Mapper %d: Error opening file %s\n", 0, j->files[f].path);  // main.c:98
+            continue;
+        }
+        std::vector<uint8_t>& d = (*j->data)[f];
+        d.resize(j->files[f].size ? j->files[f].size : 4096);
+        size_t len = 0, r;
+        while ((r = fread(d.data() + len, 1, d.size() - len, fp)) > 0) {
+            len += r;
+            if (len == d.size()) d.resize(d.size() * 2);
+        }
+        d.resize(len);
+        fclose(fp);
+    }
+    return nullptr;
+}
+}  // namespace
+
+extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, int nthreads,
+                            uint64_t hist_out[II_ALPHABET]) {
+    if (!c || (nfiles && !files)) return II_ERR_ARG;
+    std::vector<std::vector<uint8_t>> data(nfiles);
+    ReadJob job{files, nfiles, &data, 0, PTHREAD_MUTEX_INITIALIZER};
+    int nt = std::max(1, std::min(nthreads, 64));
+    std::vector<pthread_t> th(nt);
+    for (int t = 0; t < nt; t++) pthread_create(&th[t], nullptr, read_worker, &job);
+    for (int t = 0; t < nt; t++) pthread_join(th[t], nullptr);
+    std::vector<uint64_t> off(nfiles + 1, 0);
+    std::vector<uint32_t> ids(nfiles);
+    for (uint32_t f = 0; f < nfiles; f++) {
+        off[f + 1] = off[f] + data[f].size();
+        ids[f] = files[f].id0;
+    }
+    std::vector<uint8_t> text(off[nfiles] + 1);
+    for (uint32_t f = 0; f < nfiles; f++)
+        if (!data[f].empty()) memcpy(text.data() + off[f], data[f].data(), data[f].size());
+    data.clear();
+    return ii_map_host(c, text.data(), off.data(), ids.data(), nfiles, hist_out);
+}
+
+// ----------------------------------------------------------------- reduce
+static int build_dictionary(ii_ctx* c) {
+    uint64_t* counters = P_<uint64_t>(c->counters);
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    const uint32_t V = (uint32_t)c->V;
+    CK(grow(c->dslot, sizeof(uint32_t) * (V + 1)));
+    CK(grow(c->dkey, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->dkey2, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->didx, sizeof(uint32_t) * (V + 1)));
+    CK(grow(c->didx2, sizeof(uint32_t) * (V + 1)));
+    CK(grow(c->remap, sizeof(uint32_t) * c->table_cap));
+    CK(grow(c->lkey, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->lrep, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->llen, sizeof(uint32_t) * (V + 1)));
+    CK(grow(c->lstart, sizeof(uint32_t) * (II_ALPHABET + 1)));
+    CK(grow(c->tied, sizeof(uint32_t) * (V + 1)));
+
+    const unsigned long long* keys = P_<unsigned long long>(c->tkeys);
+    const uint64_t* rep = P_<uint64_t>(c->trep);
+    uint32_t* dslot = P_<uint32_t>(c->dslot);
+    CK(run_scan(c, OpCompactSlots{keys, dslot}, c->table_cap, totals + 1));
+    uint64_t vchk;
+    CK(read_u64(c, totals + 1, &vchk));
+    if (vchk != V) return II_ERR_INTERNAL;
+
+    uint64_t* sk = P_<uint64_t>(c->dkey);
+    uint64_t* sk2 = P_<uint64_t>(c->dkey2);
+    uint32_t* di = P_<uint32_t>(c->didx);
+    uint32_t* di2 = P_<uint32_t>(c->didx2);
+    k_dict_keys<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, keys, rep, dslot, V, sk, di);
+    CK(run_sort(c, &sk, &sk2, &di, &di2, V, 0, 64, false, nullptr));
+
+    // words sharing a 12-letter prefix (both longer than 12): order them by
+    // their remaining letters (LSD over 12-letter chunks on the tied subset)
+    HIPCK(hipMemsetAsync(counters + C_TIES, 0, 2 * sizeof(uint64_t), c->st));
+    k_tie_mark<<<grid_for(V), kBlock, 0, c->st>>>(sk, V, P_<uint32_t>(c->tied), counters);
+    uint64_t nt;
+    CK(read_u64(c, counters + C_TIES, &nt));
+    if (nt) {
+        CK(grow(c->tpos, sizeof(uint32_t) * nt));
+        CK(grow(c->rid, sizeof(uint32_t) * nt));
+        CK(grow(c->rfirst, sizeof(uint32_t) * nt));
+        CK(grow(c->tdict, sizeof(uint32_t) * nt));
+        CK(grow(c->tk, sizeof(uint64_t) * nt));
+        CK(grow(c->tk2, sizeof(uint64_t) * nt));
+        CK(grow(c->tv, sizeof(uint32_t) * nt));
+        CK(grow(c->tv2, sizeof(uint32_t) * nt));
+        uint32_t* tpos = P_<uint32_t>(c->tpos);
+        uint32_t* rid = P_<uint32_t>(c->rid);
+        uint32_t* rfirst = P_<uint32_t>(c->rfirst);
+        uint32_t* tdict = P_<uint32_t>(c->tdict);
+        CK(run_scan(c, OpCompactTied{P_<uint32_t>(c->tied), tpos}, V, nullptr));
+        CK(run_scan(c, OpTieRuns{tpos, sk, rid, rfirst}, nt, nullptr));
+        uint32_t* tv = P_<uint32_t>(c->tv);
+        uint32_t* tv2 = P_<uint32_t>(c->tv2);
+        uint64_t* tk = P_<uint64_t>(c->tk);
+        uint64_t* tk2 = P_<uint64_t>(c->tk2);
+        k_tie_init<<<grid_for(nt), kBlock, 0, c->st>>>(c->text, c->nbytes, tpos, (uint32_t)nt, di, dslot, rep, tdict, tv,
+                                                      counters);
+        uint64_t maxlen;
+        CK(read_u64(c, counters + C_MAXLEN, &maxlen));
+        const uint32_t kmax = (uint32_t)((maxlen + 11) / 12) - 1;  // chunks 1..kmax beyond the prefix
+        for (uint32_t ch = kmax; ch >= 1; ch--) {
+            k_tie_keys<<<grid_for(nt), kBlock, 0, c->st>>>(c->text, c->nbytes, tv, (uint32_t)nt, tdict, dslot, rep, rid,
+                                                          rfirst, ch, tk);
+            CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, 64, false, nullptr));
+        }
+        k_tie_keys<<<grid_for(nt), kBlock, 0, c->st>>>(c->text, c->nbytes, tv, (uint32_t)nt, tdict, dslot, rep, rid, rfirst,
+                                                      0, tk);
+        CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, std::max(1, bitlen(nt)), false, nullptr));
+        k_tie_place<<<grid_for(nt), kBlock, 0, c->st>>>(tk, tv, (uint32_t)nt, tpos, tdict, di);
+        HIPCK(hipGetLastError());
+    }
+    k_lex_finish<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, di, dslot, keys, rep, V, P_<uint32_t>(c->remap),
+                                                   P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen));
+    k_letter_start<<<grid_for(V + 1), kBlock, 0, c->st>>>(sk, V, P_<uint32_t>(c->lstart));
+    HIPCK(hipGetLastError());
+    // keep the sorted prefix keys in dkey for the order step
+    if (sk != P_<uint64_t>(c->dkey)) std::swap(c->dkey, c->dkey2);
+    return II_OK;
+}
+
+extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
+    if (!c) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    c->n_sc = 0;
+    const uint64_t T = c->T, V = c->V;
+    int sort_passes = 0;
+    if (T == 0) {
+        c->U = 0;
+        c->out_bytes = 0;
+        memset(c->h_letter_off, 0, sizeof(c->h_letter_off));
+        for (int e = 2; e < 8; e++) HIPCK(hipEventRecord(c->ev[e], c->st));
+        HIPCK(hipStreamSynchronize(c->st));
+        c->host_text.clear();
+        c->host_valid = copy_text != 0;
+        c->reduced = true;
+        return II_OK;
+    }
+    // ---- dictionary: lexicographic ids
+    CK(build_dictionary(c));
+    HIPCK(hipEventRecord(c->ev[2], c->st));
+
+    // ---- K2: sort records by (lexid, fid); fid order is kept by stability
+    uint64_t* r = P_<uint64_t>(c->rec);
+    uint64_t* r2 = P_<uint64_t>(c->rec2);
+    k_remap<<<(uint32_t)std::min<uint64_t>(16384, grid_for(T)), kBlock, 0, c->st>>>(r, T, P_<uint32_t>(c->remap));
+    HIPCK(hipGetLastError());
+    const int lb = std::max(1, bitlen(V - 1));
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes));
+    c->rec_sorted = r;
+    HIPCK(hipEventRecord(c->ev[3], c->st));
+
+    // ---- K3: unique (word, file) pairs and posting starts
+    CK(grow(c->uniq, sizeof(uint64_t) * T));
+    CK(grow(c->pstart, sizeof(uint64_t) * (V + 1)));
+    uint64_t* uniq = P_<uint64_t>(c->uniq);
+    uint64_t* ps = P_<uint64_t>(c->pstart);
+    CK(run_scan(c, OpUnique{r, uniq, ps}, T, ps + V));
+    CK(read_u64(c, ps + V, &c->U));
+    HIPCK(hipEventRecord(c->ev[4], c->st));
+
+    // ---- K4: final order (letter, df desc, word asc)
+    CK(grow(c->okey, sizeof(uint64_t) * V));
+    CK(grow(c->okey2, sizeof(uint64_t) * V));
+    CK(grow(c->oval, sizeof(uint32_t) * V));
+    CK(grow(c->oval2, sizeof(uint32_t) * V));
+    uint64_t* ok = P_<uint64_t>(c->okey);
+    uint64_t* ok2 = P_<uint64_t>(c->okey2);
+    uint32_t* ov = P_<uint32_t>(c->oval);
+    uint32_t* ov2 = P_<uint32_t>(c->oval2);
+    const int dbits = std::max(1, bitlen(c->nfiles_total_hint ? c->nfiles_total_hint : c->nfiles));
+    k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, (uint32_t)V, dbits, ok, ov);
+    CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr));
+    c->ord = ov;
+    HIPCK(hipEventRecord(c->ev[5], c->st));
+
+    // ---- K5: format "word:[ids]\n" lines
+    CK(grow(c->P, sizeof(uint64_t) * (c->U + 1)));
+    CK(grow(c->loff, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->letter_off, sizeof(uint64_t) * (II_ALPHABET + 1)));
+    uint64_t* Pp = P_<uint64_t>(c->P);
+    uint64_t* loff = P_<uint64_t>(c->loff);
+    CK(run_scan(c, OpPostBytes{uniq, Pp}, c->U, Pp + c->U));
+    CK(run_scan(c, OpLineOff{ov, P_<uint32_t>(c->llen), ps, Pp, loff}, V, totals + 2));
+    CK(read_u64(c, totals + 2, &c->out_bytes));
+    CK(grow(c->out, std::max<uint64_t>(c->out_bytes, 16)));
+    uint8_t* out = P_<uint8_t>(c->out);
+    k_fmt_words<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
+                                                  P_<uint32_t>(c->llen), ps, Pp, loff, (uint32_t)V, out);
+    k_fmt_posts<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(uniq, c->U, P_<uint32_t>(c->llen),
+                                                                                          ps, Pp, loff, out);
+    k_letter_off<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), ov, loff, (uint32_t)V, c->out_bytes,
+                                      P_<uint64_t>(c->letter_off));
+    HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(c->ev[6], c->st));
+    CK(read_u64(c, c->letter_off.p, c->h_letter_off, II_ALPHABET + 1));
+    if (copy_text) {
+        c->host_text.resize(c->out_bytes + 1);
+        if (c->out_bytes)
+            HIPCK(hipMemcpyAsync(c->host_text.data(), out, c->out_bytes, hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCK(hipEventRecord(c->ev[7], c->st));
+    HIPCK(hipStreamSynchronize(c->st));
+    c->host_valid = copy_text != 0;
+    c->stats.sort_passes = (uint32_t)sort_passes;
+    c->reduced = true;
+    return II_OK;
+}
+
+extern "C" int ii_letter_text(ii_ctx* c, int letter, const char** buf, size_t* len) {
+    if (!c || letter < 0 || letter >= II_ALPHABET || !buf || !len) return II_ERR_ARG;
+    if (!c->reduced || !c->host_valid) return II_ERR_STATE;
+    static const char empty[1] = {0};
+    uint64_t a = c->h_letter_off[letter], b = c->h_letter_off[letter + 1];
+    *buf = c->host_text.empty() ? empty : c->host_text.data() + a;
+    *len = (size_t)(b - a);
+    return II_OK;
+}
+
+extern "C" int ii_device_text(ii_ctx* c, const uint8_t** d_text, uint64_t letter_off[II_ALPHABET + 1]) {
+    if (!c || !d_text) return II_ERR_ARG;
+    if (!c->reduced) return II_ERR_STATE;
+    *d_text = P_<uint8_t>(c->out);
+    if (letter_off) memcpy(letter_off, c->h_letter_off, sizeof(c->h_letter_off));
+    return II_OK;
+}
+
+static double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return ms;
+}
+
+extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
+    if (!c || !o) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    ii_stats s;
+    memset(&s, 0, sizeof(s));
+    s.bytes = c->nbytes;
+    s.tokens = c->T;
+    s.words = c->V;
+    s.long_tokens = c->nlong;
+    s.table_cap = c->table_cap;
+    s.retries = c->retries;
+    memcpy(s.letter_tokens, c->hist, sizeof(c->hist));
+    s.ms_map = ev_ms(c->ev[0], c->ev[1]);
+    if (c->reduced) {
+        s.pairs = c->U;
+        s.out_bytes = c->out_bytes;
+        s.sort_passes = c->stats.sort_passes;
+        s.ms_dict = ev_ms(c->ev[1], c->ev[2]);
+        s.ms_sort = ev_ms(c->ev[2], c->ev[3]);
+        s.ms_reduce = ev_ms(c->ev[3], c->ev[4]);
+        s.ms_order = ev_ms(c->ev[4], c->ev[5]);
+        s.ms_format = ev_ms(c->ev[5], c->ev[6]);
+        s.ms_total = ev_ms(c->ev[0], c->ev[6]);
+        double sum = 0;
+        for (int i = 0; i < c->n_sc; i++) sum += ev_ms(c->ev_sc[2 * i], c->ev_sc[2 * i + 1]);
+        s.scatter_launches = (uint32_t)c->n_sc;
+        s.scatter_ms_avg = c->n_sc ? sum / c->n_sc : 0;
+        s.scatter_bytes = 16ull * c->T;  // read 8 B + write 8 B per record
+    }
+    *o = s;
+    return II_OK;
+}
+
+// ----------------------------------------------------------------- host helpers
+extern "C" int ii_reducer_letters(int r, int R, int* lo, int* hi) {
+    if (R < 1 || r < 0 || r >= R || !lo || !hi) return II_ERR_ARG;
+    *lo = (II_ALPHABET / R) * r;                                       // main.c:129
+    *hi = (r == R - 1) ? II_ALPHABET : (II_ALPHABET / R) * (r + 1);    // main.c:130
+    return II_OK;
+}
+
+extern "C" int ii_partition(const uint64_t* sizes, uint32_t nfiles, int M, uint32_t* order, uint32_t* shard_begin,
+                            uint32_t* shard_end) {
+    if (M < 1 || (nfiles && (!sizes || !order)) || !shard_begin || !shard_end) return II_ERR_ARG;
+    for (uint32_t i = 0; i < nfiles; i++) order[i] = i;
+    // size descending (main.c:21-25, 300); ties by list position (stable)
+    std::stable_sort(order, order + nfiles, [&](uint32_t a, uint32_t b) { return sizes[a] > sizes[b]; });
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nfiles; i++) total += sizes[i];
+    const uint64_t per = total / (uint64_t)M;  // main.c:307
+    for (int m = 0; m < M; m++) shard_begin[m] = shard_end[m] = nfiles;
+    int cur = 0;
+    uint64_t cum = 0;
+    shard_begin[0] = 0;
+    for (uint32_t i = 0; i < nfiles; i++) {  // main.c:315-322
+        cum += sizes[order[i]];
+        if (cum >= per && cur < M - 1) {
+            shard_end[cur] = i + 1;
+            shard_begin[++cur] = i + 1;
+            cum = 0;
+        }
+    }
+    shard_end[cur] = nfiles;  // main.c:323
+    for (int m = cur + 1; m < M; m++) shard_begin[m] = shard_end[m] = nfiles;  // defined: empty shards
+    return II_OK;
+}

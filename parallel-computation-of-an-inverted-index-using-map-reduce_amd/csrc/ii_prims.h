@@ -1,0 +1,255 @@
+// ii_prims.h — device-wide primitives for the MI355X inverted-index pipeline:
+// exclusive scan and a stable LSD radix sort, both written for wave64 / gfx950.
+//
+// Both use the "reduce-then-scan" structure with NO inter-workgroup
+// communication inside a launch: every workgroup owns one contiguous chunk of
+// the input, a first kernel reduces each chunk, a one-workgroup kernel scans
+// the per-chunk results, and a third kernel re-reads its chunk and writes.
+// Chunks are processed tile by tile in order, so the radix sort is stable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ii {
+
+constexpr int kBlock = 256;           // threads per workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxChunks = 2048;      // workgroups of a reduce-then-scan launch
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    return (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+}
+
+// Inclusive wave64 scan of a u64 value.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t t = __shfl_up(v, o, 64);
+        if (lane_id() >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive block scan (256 threads); returns the exclusive prefix and the block total.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total, uint64_t* lds /*kWaves+1*/) {
+    uint64_t inc = wave_incl_scan(v);
+    if (lane_id() == 63) lds[wave_id()] = inc;
+    __syncthreads();
+    uint64_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        uint64_t s = lds[w];
+        if (w < wave_id()) wbase += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + inc - v;
+}
+
+// ----------------------------------------------------------------------------
+// Device-wide exclusive scan over n items.  Op provides
+//   uint64_t value(uint64_t i)                 (the item)
+//   void     emit(uint64_t i, uint64_t excl, uint64_t value)
+// Items are handled per chunk; per-chunk sums land in `partial`.
+// ----------------------------------------------------------------------------
+template <class Op>
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(Op op, uint64_t n, uint64_t chunk, uint64_t* partial) {
+    __shared__ uint64_t lds[kWaves + 1];
+    uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint64_t acc = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) acc += op.value(i);
+    acc = wave_sum(acc);
+    if (lane_id() == 0) lds[wave_id()] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < kWaves; w++) t += lds[w];
+        partial[blockIdx.x] = t;
+    }
+}
+
+// One workgroup: exclusive scan of m <= kMaxChunks values in place; total -> *total.
+__global__ __launch_bounds__(kBlock) void k_scan_partials(uint64_t* partial, uint32_t m, uint64_t* total) {
+    __shared__ uint64_t lds[kWaves + 1];
+    constexpr int kPer = kMaxChunks / kBlock;  // 8 values per thread
+    uint64_t v[kPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        uint32_t i = threadIdx.x * kPer + j;
+        v[j] = i < m ? partial[i] : 0;
+        s += v[j];
+    }
+    uint64_t tot;
+    uint64_t ex = block_excl_scan(s, &tot, lds);
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        uint32_t i = threadIdx.x * kPer + j;
+        if (i < m) partial[i] = ex;
+        ex += v[j];
+    }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
+
+template <class Op>
+__global__ __launch_bounds__(kBlock) void k_scan_apply(Op op, uint64_t n, uint64_t chunk, const uint64_t* partial) {
+    __shared__ uint64_t lds[kWaves + 1];
+    uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint64_t run = partial[blockIdx.x];
+    for (uint64_t base = lo; base < hi; base += kBlock) {
+        uint64_t i = base + threadIdx.x;
+        uint64_t v = i < hi ? op.value(i) : 0;
+        uint64_t tot;
+        uint64_t ex = block_excl_scan(v, &tot, lds);
+        if (i < hi) op.emit(i, run + ex, v);
+        run += tot;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Stable LSD radix sort, 8-bit digits.  Keys u64 (digit taken from bits
+// [shift, shift+8)), optional u32 payload.  Each pass: histogram per chunk
+// (digit-major table), exclusive scan of the table, stable scatter.
+// ----------------------------------------------------------------------------
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;
+constexpr int kSortItems = 16;                     // keys per thread per tile
+constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
+
+// Digit extraction functor for a plain key array.
+struct DigitOf {
+    int shift;
+    __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)(k >> shift) & (kRadix - 1); }
+};
+
+// Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
+// one exclusive scan of the table yields every chunk's scatter base).
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
+                                                       int shift, uint32_t nchunks, uint64_t* __restrict__ table) {
+    __shared__ uint32_t cnt[kWaves][kRadix];
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint32_t* mine = cnt[wave_id()];
+    // two keys per lane per step (16 B per lane)
+    uint64_t i = lo + 2 * threadIdx.x;
+    for (; i + 1 < hi; i += 2 * kBlock) {
+        uint64_t a = keys[i], b = keys[i + 1];
+        atomicAdd(&mine[(uint32_t)(a >> shift) & (kRadix - 1)], 1u);
+        atomicAdd(&mine[(uint32_t)(b >> shift) & (kRadix - 1)], 1u);
+    }
+    if (i < hi) atomicAdd(&mine[(uint32_t)(keys[i] >> shift) & (kRadix - 1)], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < kRadix; d += kBlock) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) t += cnt[w][d];
+        table[(uint64_t)d * nchunks + blockIdx.x] = t;
+    }
+}
+
+// Stable scatter.  Tile layout: thread (wave w, lane l) holds items k at
+// tile_base + w*64*kSortItems + k*64 + l, so (w, k, l) order == index order.
+// Ranks inside a wave come from a 64-lane match on the digit (8 ballots);
+// the tile is reordered by digit in LDS and written out in runs.
+template <bool kHasVals>
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                          const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
+                                                          uint64_t n, uint64_t chunk, int shift, uint32_t nchunks,
+                                                          const uint64_t* __restrict__ table) {
+    __shared__ uint64_t s_keys[kSortTile];
+    __shared__ uint32_t s_vals[kHasVals ? kSortTile : 1];
+    __shared__ uint32_t s_wcnt[kWaves][kRadix];
+    __shared__ uint32_t s_tstart[kRadix];
+    __shared__ uint64_t s_run[kRadix];
+    __shared__ uint64_t s_scan[kWaves + 1];
+    static_assert(kRadix == kBlock, "one digit per thread");
+
+    const int w = wave_id(), l = lane_id(), t = threadIdx.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
+    const uint64_t lt = lanemask_lt();
+
+    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ww++) s_wcnt[ww][t] = 0;
+        __syncthreads();
+        uint64_t key[kSortItems];
+        uint32_t val[kSortItems];
+        uint32_t rank[kSortItems];
+        const uint64_t wbase = tb + (uint64_t)w * 64 * kSortItems + l;
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            uint64_t idx = wbase + (uint64_t)k * 64;
+            bool valid = idx < hi;
+            key[k] = valid ? kin[idx] : ~0ull;
+            if (kHasVals) val[k] = valid ? vin[idx] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const bool valid = wbase + (uint64_t)k * 64 < hi;
+            const uint32_t d = (uint32_t)(key[k] >> shift) & (kRadix - 1);
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < kRadixBits; b++) {
+                const bool bit = (d >> b) & 1;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            uint32_t r = 0;
+            if (valid) {
+                const uint32_t before = s_wcnt[w][d];
+                r = before + __popcll(m & lt);
+                if ((m & lt) == 0) s_wcnt[w][d] = before + __popcll(m);
+            }
+            rank[k] = r;
+        }
+        __syncthreads();
+        // digit t: totals, tile start, per-wave offsets
+        uint32_t c0 = s_wcnt[0][t], c1 = s_wcnt[1][t], c2 = s_wcnt[2][t], c3 = s_wcnt[3][t];
+        uint32_t tot_d = c0 + c1 + c2 + c3;
+        uint64_t all;
+        uint32_t start = (uint32_t)block_excl_scan(tot_d, &all, s_scan);
+        s_tstart[t] = start;
+        s_wcnt[0][t] = start;
+        s_wcnt[1][t] = start + c0;
+        s_wcnt[2][t] = start + c0 + c1;
+        s_wcnt[3][t] = start + c0 + c1 + c2;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            if (wbase + (uint64_t)k * 64 < hi) {
+                const uint32_t d = (uint32_t)(key[k] >> shift) & (kRadix - 1);
+                const uint32_t pos = s_wcnt[w][d] + rank[k];
+                s_keys[pos] = key[k];
+                if (kHasVals) s_vals[pos] = val[k];
+            }
+        }
+        __syncthreads();
+        const uint32_t tile_n = (uint32_t)((hi - tb) < (uint64_t)kSortTile ? (hi - tb) : (uint64_t)kSortTile);
+#pragma unroll
+        for (int j = 0; j < kSortItems; j++) {
+            const uint32_t p = j * kBlock + t;
+            if (p < tile_n) {
+                const uint64_t k = s_keys[p];
+                const uint32_t d = (uint32_t)(k >> shift) & (kRadix - 1);
+                const uint64_t dst = s_run[d] + (p - s_tstart[d]);
+                kout[dst] = k;
+                if (kHasVals) vout[dst] = s_vals[p];
+            }
+        }
+        __syncthreads();
+        s_run[t] += tot_d;
+        // the next iteration's first __syncthreads orders this update before use
+    }
+}
+
+}  // namespace ii

@@ -1,0 +1,38 @@
+"""ctypes access to the C oracle (oracle/ii_oracle.c) — TEST INFRASTRUCTURE ONLY.
+The oracle is the parity checker; it is never part of the product path."""
+import ctypes
+import os
+
+_ORACLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "build",
+                       "libii_oracle.so")
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(_ORACLE)
+        _lib.ii_oracle_index.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+        _lib.ii_oracle_free.argtypes = [ctypes.c_void_p]
+    return _lib
+
+
+def oracle_index(text, file_off, file_id0):
+    """-> {letter: bytes} exactly as the reference would write a.txt..z.txt."""
+    import numpy as np
+    L = _load()
+    if hasattr(text, "ctypes"):
+        tb = np.ascontiguousarray(text, dtype=np.uint8)
+    else:
+        tb = np.frombuffer(bytes(text), dtype=np.uint8)
+    off = np.ascontiguousarray(np.asarray(file_off, dtype=np.uint64))
+    ids = np.ascontiguousarray(np.asarray(file_id0, dtype=np.uint32))
+    out = ctypes.c_void_p()
+    loff = (ctypes.c_uint64 * 27)()
+    rc = L.ii_oracle_index(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
+                           ctypes.byref(out), loff)
+    assert rc == 0
+    res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
+    L.ii_oracle_free(out)
+    return res

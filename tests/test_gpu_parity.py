@@ -1,0 +1,158 @@
+"""GPU parity: the MI355X path (libii.so through the C ABI and the ii_index
+CLI) against the reference's golden outputs and the oracle, bit-exact."""
+import os
+import random
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import ii_ctypes
+from conftest import CASES, PKG, case_arrays, materialize
+from oracle_py import oracle_index
+
+pytestmark = pytest.mark.gpu
+LETTERS = "abcdefghijklmnopqrstuvwxyz"
+
+
+@pytest.fixture(scope="module")
+def idx():
+    ix = ii_ctypes.Index(0)
+    yield ix
+    ix.close()
+
+
+def assert_same(got, expected, ctx=""):
+    for l in LETTERS:
+        if got[l] != expected[l]:
+            a, b = got[l], expected[l]
+            i = next((k for k in range(min(len(a), len(b))) if a[k] != b[k]), min(len(a), len(b)))
+            raise AssertionError("%s letter %s differs at byte %d: got %r expected %r" %
+                                 (ctx, l, i, a[max(0, i - 40):i + 40], b[max(0, i - 40):i + 40]))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_cli_matches_reference(case):
+    with tempfile.TemporaryDirectory() as td:
+        _, _, expected = materialize(case, td)
+        r = subprocess.run([os.path.join(PKG, "ii_index"), "3", "5", "list.txt"], cwd=td, capture_output=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr.decode()
+        got = {l: open(os.path.join(td, l + ".txt"), "rb").read() for l in LETTERS}
+        assert_same(got, expected, case)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_map_host_matches_reference(idx, case):
+    text, off, ids, expected = case_arrays(case)
+    hist = idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), expected, case)
+    st = idx.stats()
+    assert sum(hist) == st.tokens
+    lines = {l: expected[l].count(b"\n") for l in LETTERS}
+    for i, l in enumerate(LETTERS):
+        assert (hist[i] == 0) == (lines[l] == 0)
+    assert st.words == sum(lines.values())
+    assert st.out_bytes == sum(len(v) for v in expected.values())
+
+
+def test_map_device_torch_buffer(idx):
+    import torch
+    text, off, ids, expected = case_arrays("config2")
+    # build the device layout: separator after each file (contract of ii_map_device)
+    buf = bytearray()
+    starts = []
+    for f in range(len(ids)):
+        starts.append(len(buf))
+        buf += text[off[f]:off[f + 1]] + b"\n"
+    d = torch.tensor(np.frombuffer(bytes(buf), dtype=np.uint8), device="cuda")
+    torch.cuda.synchronize()
+    idx.map_device(d.data_ptr(), len(buf), starts, ids)
+    idx.reduce()
+    assert_same(idx.letters(), expected, "device")
+
+
+def test_map_device_layout_violation(idx):
+    import torch
+    d = torch.tensor(np.frombuffer(b"abc def", dtype=np.uint8), device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(ii_ctypes.IIError) as e:
+        idx.map_device(d.data_ptr(), 7, [0, 2], [0, 1])  # file 1 starts mid-token
+    assert e.value.code == -6
+
+
+def test_empty_inputs(idx):
+    for text, off, ids in [(b"", [0], []), (b"", [0, 0, 0], [0, 1]), (b"123 ,,, \n\t 456", [0, 15], [0]),
+                           (b" \x00abc ", [0, 6], [0])]:
+        idx.map_host(text, off, ids)
+        idx.reduce()
+        got = idx.letters()
+        assert all(v == b"" for v in got.values())
+
+
+def rand_corpus(seed, nfiles, max_bytes):
+    rng = random.Random(seed)
+    letters = b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"
+    other = b"0123456789.,'-_\x00\x80\xc3\xa9\xff\x1c\x85\xa0"
+    spaces = b" \t\n\x0b\x0c\r"
+    vocab = [bytes(rng.choice(letters) for _ in range(rng.choice([1, 2, 3, 5, 8, 12, 13, 15, 24, 25, 40])))
+             for _ in range(300)]
+    text = bytearray()
+    off = [0]
+    for _ in range(nfiles):
+        n = rng.randint(0, max_bytes)
+        f = bytearray()
+        while len(f) < n:
+            t = bytearray(rng.choice(vocab))
+            for _ in range(rng.choice([0, 0, 1, 2])):
+                t.insert(rng.randint(0, len(t)), rng.choice(other))
+            if rng.random() < 0.002:
+                t = bytearray(rng.choice(letters) for _ in range(rng.randint(250, 700)))  # beyond 299: defined UB
+            f += t + bytes([rng.choice(spaces)])
+        if rng.random() < 0.5:
+            f = f.rstrip(spaces)
+        text += f
+        off.append(len(text))
+    return bytes(text), off, list(range(nfiles))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_corpora_vs_oracle(idx, seed):
+    text, off, ids = rand_corpus(seed, [5, 50, 200, 900][seed - 1], [200000, 30000, 3000, 400][seed - 1])
+    idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(text, off, ids), "seed %d" % seed)
+
+
+def test_noncontiguous_ids(idx):
+    # a shard: files with gaps in their IDs (multi-GPU shards, missing files)
+    text, off, _ = rand_corpus(9, 40, 5000)
+    ids = [3 * i + 7 for i in range(40)]
+    idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(text, off, ids), "ids")
+
+
+def test_table_regrow_and_reuse():
+    os.environ["II_TABLE_LOG2"] = "10"  # 1024 slots: forces several regrows
+    try:
+        ix = ii_ctypes.Index(0)
+    finally:
+        del os.environ["II_TABLE_LOG2"]
+    text, off, ids, expected = case_arrays("zipf_small")
+    for _ in range(2):
+        ix.map_host(text, off, ids)
+        ix.reduce()
+        assert_same(ix.letters(), expected, "regrow")
+    assert ix.stats().table_cap >= 2 * ix.stats().words
+    ix.close()
+
+
+def test_zipf_medium_vs_oracle(idx):
+    t, off = ii_ctypes.zipf_corpus(48_000_000, 700, 300_000, 21, threads=8)
+    ids = list(range(700))
+    idx.map_host(t, off.tolist(), ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(t, off, ids), "zipf48M")

@@ -1,0 +1,52 @@
+"""CPU: the oracle (C restatement, oracle/ii_oracle.c) is pinned against the
+reference binary's own outputs (tests/golden/, made by make_golden.py)."""
+import hashlib
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import CASES, GOLDEN, ORACLE, case_arrays, materialize
+from oracle_py import oracle_index
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_matches_reference_goldens(case):
+    text, off, ids, expected = case_arrays(case)
+    got = oracle_index(text, off, ids)
+    for l in "abcdefghijklmnopqrstuvwxyz":
+        assert got[l] == expected[l], "letter %s differs" % l
+
+
+def test_golden_json_consistent():
+    meta = json.load(open(os.path.join(GOLDEN, "golden.json")))
+    # config 1 / config 2 aggregate hashes of the reference
+    assert meta["cases"]["config1"]["sha256"].startswith("8968c9ae0ce82a20")
+    assert meta["cases"]["config2"]["sha256"].startswith("47a8ad1e4b6f28c3")
+    assert meta["cases"]["config2"]["lines"] == 33262
+    assert meta["cases"]["config2"]["out_bytes"] == 1380621
+    for case in CASES:
+        _, _, _, expected = case_arrays(case)
+        allb = b"".join(expected[l] for l in "abcdefghijklmnopqrstuvwxyz")
+        assert hashlib.sha256(allb).hexdigest() == meta["cases"][case]["sha256"]
+
+
+@pytest.mark.parametrize("case", ["config1", "edge", "tiny360"])
+def test_oracle_cli_matches(case):
+    with tempfile.TemporaryDirectory() as td:
+        _, _, expected = materialize(case, td)
+        subprocess.run([os.path.join(ORACLE, "build", "ii_oracle"), "2", "3", "list.txt"], cwd=td, check=True,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        for l in "abcdefghijklmnopqrstuvwxyz":
+            assert open(os.path.join(td, l + ".txt"), "rb").read() == expected[l]
+
+
+def test_oracle_defined_ub_long_token():
+    # raw token >= 300 bytes: reference UB (stack overflow); defined as keeping
+    # the first 299 letters
+    text = b"A" * 500 + b" b"
+    got = oracle_index(text, [0, len(text)], [0])
+    assert got["a"] == b"a" * 299 + b":[1]\n"
+    assert got["b"] == b"b:[1]\n"
