@@ -12,7 +12,9 @@ steps (every step re-tokenizes and rebuilds the index from scratch).
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
-indexes its own 10 GB corpus (weak scaling).  Rank 0 prints ONE JSON line.
+indexes its own 10 GB corpus (weak scaling): map + local reduce on its shard,
+one RCCL all-to-allv of letter ranges (ii_dist.exchange_and_reduce), and the
+owner's merge + order + format.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes
@@ -110,6 +112,7 @@ def main():
     import torch
     import torch.distributed as dist
     import ii_ctypes
+    import ii_dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -135,9 +138,14 @@ def main():
 
     idx = ii_ctypes.Index(local if world > 1 else 0)
 
+    id_bound = world * a.files
+
     def step():
         idx.map_device(d_text.data_ptr(), nbytes, file_start, ids)
-        idx.reduce(copy_text=False)
+        if world > 1:  # local reduce -> letter-range all-to-allv (RCCL) -> owner merge + format
+            ii_dist.exchange_and_reduce(idx, id_bound)
+        else:
+            idx.reduce(copy_text=False)
 
     for _ in range(a.warmup):
         step()

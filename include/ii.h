@@ -124,6 +124,34 @@ int ii_map_device(ii_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uin
  */
 int ii_reduce(ii_ctx *ctx, int copy_text);
 
+/* First half of ii_reduce: distinct (word, file) pairs grouped by word — the
+ * state the reducers reach after main.c:170-213, for this context's files.
+ * Needed explicitly only before ii_export_plan (ii_reduce runs it itself). */
+int ii_reduce_local(ii_ctx *ctx);
+
+/*
+ * Multi-GPU exchange.  The reference assigns first-letter
+ * ranges to reducers (main.c:129-130); with G GPUs, GPU r owns the letters
+ * ii_reducer_letters(r, G).  Each GPU maps its shard of files, then:
+ *   ii_export_plan  -> bytes of the segment for every owner (host array)
+ *   ii_export       -> writes the segments into a device send buffer at the
+ *                      caller's (8-byte aligned) offsets
+ *   (caller moves segment r of every GPU to GPU r: RCCL all-to-allv)
+ *   ii_import       -> merges the G received segments (one per source, in
+ *                      source order) into this context's partial index
+ *   ii_reduce       -> orders and formats the owner's letters
+ * Segment layout (little-endian, 8-byte aligned):
+ *   u64 header[8] = {magic "IXIISEG1", nwords, npairs, arena_bytes,
+ *                    letter_lo, letter_hi, 0, 0}
+ *   u64 pairs[npairs] = (word index in segment) << 32 | id0
+ *   u8  arena[arena_bytes rounded up to 8] = words in lexicographic order,
+ *                    each followed by ' '
+ * id_bound = 1 + the largest id0 of all files of all GPUs.
+ */
+int ii_export_plan(ii_ctx *ctx, int nparts, uint64_t *seg_bytes);
+int ii_export(ii_ctx *ctx, int nparts, void *d_send, const uint64_t *send_off);
+int ii_import(ii_ctx *ctx, int nparts, const void *d_recv, const uint64_t *recv_off, uint32_t id_bound);
+
 /* Text of <letter>.txt (letter 0..25 = 'a'..'z'), valid until the next call. */
 int ii_letter_text(ii_ctx *ctx, int letter, const char **buf, size_t *len);
 

@@ -51,9 +51,21 @@ class IIFile(ctypes.Structure):
 _lib = None
 
 
+def _init_torch_first():
+    """torch ships its own libamdhip64; whichever HIP runtime initialises first
+    owns the device in this process.  When torch is importable, let it
+    initialise first so libii.so binds to the same runtime (same soname)."""
+    try:
+        import torch
+        torch.cuda.is_available()
+    except Exception:
+        pass
+
+
 def lib():
     global _lib
     if _lib is None:
+        _init_torch_first()
         path = os.path.join(PKG_DIR, "libii.so")
         if not os.path.exists(path):
             raise FileNotFoundError("libii.so not built (make -C %s)" % PKG_DIR)
@@ -77,6 +89,10 @@ def lib():
         L.ii_reducer_letters.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                          ctypes.POINTER(ctypes.c_int)]
         L.ii_partition.argtypes = [u64p, ctypes.c_uint32, ctypes.c_int, u32p, u32p, u32p]
+        L.ii_reduce_local.argtypes = [ctypes.c_void_p]
+        L.ii_export_plan.argtypes = [ctypes.c_void_p, ctypes.c_int, u64p]
+        L.ii_export.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, u64p]
+        L.ii_import.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, u64p, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -144,6 +160,20 @@ class Index:
 
     def reduce(self, copy_text=True):
         _check(lib().ii_reduce(self.h, 1 if copy_text else 0), "ii_reduce")
+
+    def reduce_local(self):
+        _check(lib().ii_reduce_local(self.h), "ii_reduce_local")
+
+    def export_plan(self, nparts):
+        out = (ctypes.c_uint64 * nparts)()
+        _check(lib().ii_export_plan(self.h, nparts, out), "ii_export_plan")
+        return list(out)
+
+    def export(self, nparts, d_send_ptr, send_off):
+        _check(lib().ii_export(self.h, nparts, ctypes.c_void_p(d_send_ptr), _u64(send_off)), "ii_export")
+
+    def import_(self, nparts, d_recv_ptr, recv_off, id_bound):
+        _check(lib().ii_import(self.h, nparts, ctypes.c_void_p(d_recv_ptr), _u64(recv_off), id_bound), "ii_import")
 
     def letter_text(self, letter):
         buf = ctypes.c_char_p()

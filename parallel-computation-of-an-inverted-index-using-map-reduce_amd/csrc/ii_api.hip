@@ -36,7 +36,7 @@ struct ii_ctx {
     const uint8_t* text = nullptr;
     uint64_t nbytes = 0;
     uint32_t nfiles = 0;
-    uint32_t nfiles_total_hint = 0;  // upper bound of df when shards are merged
+    uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df and the id sort bits)
     DBuf fstart, fid;
 
     // scratch
@@ -52,10 +52,14 @@ struct ii_ctx {
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
     DBuf uniq, pstart, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    // exchange
+    DBuf woff, pts;
+    uint64_t h_pts[3 * (II_ALPHABET + 1)] = {0};
+    int planned_parts = 0;
 
     uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
     uint32_t retries = 0;
-    bool mapped = false, reduced = false;
+    bool mapped = false, have_pairs = false, reduced = false;
     uint64_t* rec_sorted = nullptr;
     uint32_t* ord = nullptr;
     uint64_t hist[II_ALPHABET] = {0};
@@ -213,7 +217,8 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->dkey,     &c->dkey2,  &c->didx,  &c->didx2,   &c->remap,  &c->lkey,     &c->lrep,
                    &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
-                   &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off};
+                   &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
+                   &c->woff,     &c->pts};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -241,7 +246,8 @@ extern "C" const char* ii_strerror(int code) {
 
 // ----------------------------------------------------------------- map (K1)
 static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
-    c->mapped = c->reduced = false;
+    c->mapped = c->have_pairs = c->reduced = false;
+    c->planned_parts = 0;
     c->host_valid = false;
     c->n_sc = 0;
     c->retries = 0;
@@ -344,6 +350,7 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
         HIPCK(hipStreamSynchronize(c->st));  // caller's host arrays may go away after return
     }
     c->nfiles = nfiles;
+    c->id_bound = nfiles ? file_id0[nfiles - 1] + 1 : 0;
     return II_OK;
 }
 
@@ -526,23 +533,19 @@ static int build_dictionary(ii_ctx* c) {
     return II_OK;
 }
 
-extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
-    if (!c) return II_ERR_ARG;
-    if (!c->mapped) return II_ERR_STATE;
-    HIPCK(hipSetDevice(c->dev));
+// Local reduce: dictionary (lexicographic ids), K2 token sort, K3 unique
+// pairs.  After it the context holds a partial index: uniq (lexid, id0)
+// pairs grouped by word, post_start, and the per-word dictionary arrays.
+static int local_reduce(ii_ctx* c) {
     uint64_t* totals = P_<uint64_t>(c->totals);
+    (void)totals;
     c->n_sc = 0;
     const uint64_t T = c->T, V = c->V;
     int sort_passes = 0;
     if (T == 0) {
         c->U = 0;
-        c->out_bytes = 0;
-        memset(c->h_letter_off, 0, sizeof(c->h_letter_off));
-        for (int e = 2; e < 8; e++) HIPCK(hipEventRecord(c->ev[e], c->st));
-        HIPCK(hipStreamSynchronize(c->st));
-        c->host_text.clear();
-        c->host_valid = copy_text != 0;
-        c->reduced = true;
+        c->have_pairs = true;
+        for (int e = 2; e < 5; e++) HIPCK(hipEventRecord(c->ev[e], c->st));
         return II_OK;
     }
     // ---- dictionary: lexicographic ids
@@ -567,7 +570,27 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     CK(run_scan(c, OpUnique{r, uniq, ps}, T, ps + V));
     CK(read_u64(c, ps + V, &c->U));
     HIPCK(hipEventRecord(c->ev[4], c->st));
+    c->stats.sort_passes = (uint32_t)sort_passes;
+    c->have_pairs = true;
+    return II_OK;
+}
 
+// K4 final order + K5 formatting of the partial index held by the context.
+static int order_and_format(ii_ctx* c, int copy_text) {
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    const uint64_t V = c->V;
+    if (c->U == 0 || V == 0) {
+        c->out_bytes = 0;
+        memset(c->h_letter_off, 0, sizeof(c->h_letter_off));
+        for (int e = 5; e < 8; e++) HIPCK(hipEventRecord(c->ev[e], c->st));
+        HIPCK(hipStreamSynchronize(c->st));
+        c->host_text.clear();
+        c->host_valid = copy_text != 0;
+        c->reduced = true;
+        return II_OK;
+    }
+    uint64_t* uniq = P_<uint64_t>(c->uniq);
+    uint64_t* ps = P_<uint64_t>(c->pstart);
     // ---- K4: final order (letter, df desc, word asc)
     CK(grow(c->okey, sizeof(uint64_t) * V));
     CK(grow(c->okey2, sizeof(uint64_t) * V));
@@ -577,7 +600,7 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     uint64_t* ok2 = P_<uint64_t>(c->okey2);
     uint32_t* ov = P_<uint32_t>(c->oval);
     uint32_t* ov2 = P_<uint32_t>(c->oval2);
-    const int dbits = std::max(1, bitlen(c->nfiles_total_hint ? c->nfiles_total_hint : c->nfiles));
+    const int dbits = std::max(1, bitlen(c->id_bound));
     k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, (uint32_t)V, dbits, ok, ov);
     CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr));
     c->ord = ov;
@@ -611,8 +634,168 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     HIPCK(hipEventRecord(c->ev[7], c->st));
     HIPCK(hipStreamSynchronize(c->st));
     c->host_valid = copy_text != 0;
-    c->stats.sort_passes = (uint32_t)sort_passes;
     c->reduced = true;
+    return II_OK;
+}
+
+extern "C" int ii_reduce_local(ii_ctx* c) {
+    if (!c) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    if (c->have_pairs) return II_OK;
+    return local_reduce(c);
+}
+
+extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
+    if (!c) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    if (!c->have_pairs) CK(local_reduce(c));
+    return order_and_format(c, copy_text);
+}
+
+// ----------------------------------------------------------------- exchange
+// Per-letter points of the partial index (first word / pair / arena byte).
+static int letter_points(ii_ctx* c) {
+    const uint64_t V = c->V;
+    if (V == 0 || c->T == 0) {
+        memset(c->h_pts, 0, sizeof(c->h_pts));
+        return II_OK;
+    }
+    CK(grow(c->woff, sizeof(uint64_t) * (V + 1)));
+    CK(grow(c->pts, sizeof(uint64_t) * 3 * (II_ALPHABET + 1)));
+    uint64_t* woff = P_<uint64_t>(c->woff);
+    CK(run_scan(c, OpWordArena{P_<uint32_t>(c->llen), woff}, V, woff + V));
+    k_letter_points<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), P_<uint64_t>(c->pstart), woff, P_<uint64_t>(c->pts));
+    HIPCK(hipGetLastError());
+    CK(read_u64(c, c->pts.p, c->h_pts, 3 * (II_ALPHABET + 1)));
+    return II_OK;
+}
+
+static inline uint64_t seg_bytes(uint64_t nw, uint64_t np, uint64_t arena) {
+    (void)nw;
+    return 64 + 8 * np + ((arena + 7) & ~7ull);
+}
+
+extern "C" int ii_export_plan(ii_ctx* c, int nparts, uint64_t* bytes_out) {
+    if (!c || nparts < 1 || !bytes_out) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    if (!c->have_pairs) CK(local_reduce(c));
+    CK(letter_points(c));
+    for (int r = 0; r < nparts; r++) {
+        int lo, hi;
+        ii_reducer_letters(r, nparts, &lo, &hi);
+        const uint64_t* a = c->h_pts + 3 * lo;
+        const uint64_t* b = c->h_pts + 3 * hi;
+        bytes_out[r] = seg_bytes(b[0] - a[0], b[1] - a[1], b[2] - a[2]);
+    }
+    c->planned_parts = nparts;
+    return II_OK;
+}
+
+extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* send_off) {
+    if (!c || nparts < 1 || !d_send || !send_off) return II_ERR_ARG;
+    if (c->planned_parts != nparts) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    for (int r = 0; r < nparts; r++) {
+        if (send_off[r] & 7) return II_ERR_ARG;
+        int lo, hi;
+        ii_reducer_letters(r, nparts, &lo, &hi);
+        const uint64_t* a = c->h_pts + 3 * lo;
+        const uint64_t* b = c->h_pts + 3 * hi;
+        const uint64_t nw = b[0] - a[0], np = b[1] - a[1], ab = b[2] - a[2];
+        uint8_t* seg = (uint8_t*)d_send + send_off[r];
+        uint64_t* pairs = (uint64_t*)(seg + 64);
+        uint8_t* arena = seg + 64 + 8 * np;
+        k_export_header<<<1, 64, 0, c->st>>>((uint64_t*)seg, nw, np, ab, lo, hi);
+        if (np)
+            k_export_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
+                P_<uint64_t>(c->uniq), a[1], b[1], (uint32_t)a[0], pairs);
+        if (nw)
+            k_export_words<<<grid_for(nw), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey),
+                                                              P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen),
+                                                              P_<uint64_t>(c->woff), (uint32_t)a[0], (uint32_t)b[0],
+                                                              arena);
+        HIPCK(hipGetLastError());
+    }
+    HIPCK(hipStreamSynchronize(c->st));
+    return II_OK;
+}
+
+extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64_t* recv_off, uint32_t id_bound) {
+    if (!c || nparts < 1 || !recv_off || (!d_recv && nparts)) return II_ERR_ARG;
+    HIPCK(hipSetDevice(c->dev));
+    std::vector<uint64_t> hdr(8 * (size_t)nparts);
+    for (int s = 0; s < nparts; s++) {
+        if (recv_off[s] & 7) return II_ERR_ARG;
+        HIPCK(hipMemcpyAsync(&hdr[8 * s], (const uint8_t*)d_recv + recv_off[s], 64, hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCK(hipStreamSynchronize(c->st));
+    uint64_t W = 0, NP = 0, A = 0;
+    for (int s = 0; s < nparts; s++) {
+        if (hdr[8 * s] != kSegMagic) return II_ERR_ARG;
+        W += hdr[8 * s + 1];
+        NP += hdr[8 * s + 2];
+        A += hdr[8 * s + 3];
+    }
+    // merged word text: every source's words, in source order
+    CK(grow(c->text_own, std::max<uint64_t>(A, 16)));
+    uint64_t o = 0;
+    for (int s = 0; s < nparts; s++) {
+        const uint64_t np = hdr[8 * s + 2], ab = hdr[8 * s + 3];
+        if (ab)
+            HIPCK(hipMemcpyAsync((uint8_t*)c->text_own.p + o, (const uint8_t*)d_recv + recv_off[s] + 64 + 8 * np, ab,
+                                 hipMemcpyDeviceToDevice, c->st));
+        o += ab;
+    }
+    CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>({W, NP, 1})));
+    CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>({W, NP, 1})));
+    c->text = P_<uint8_t>(c->text_own);
+    c->nbytes = A;
+    const uint64_t fs0 = 0;
+    const uint32_t id0 = 0;
+    CK(set_files(c, &fs0, &id0, A ? 1 : 0));
+    CK(map_core(c, nullptr));  // tokenises the words: word k -> rec[k] = slot << 32
+    if (c->T != W) return II_ERR_INTERNAL;
+    c->id_bound = id_bound;
+    if (W == 0) {
+        c->T = 0;
+        c->U = 0;
+        c->have_pairs = true;
+        return II_OK;
+    }
+    CK(build_dictionary(c));
+    HIPCK(hipEventRecord(c->ev[2], c->st));
+    uint64_t* wrec = P_<uint64_t>(c->rec);
+    uint64_t* r = P_<uint64_t>(c->rec2);
+    uint64_t* r2 = P_<uint64_t>(c->rec);
+    uint64_t wbase = 0, pbase = 0;
+    for (int s = 0; s < nparts; s++) {
+        const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
+        if (np)
+            k_import_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
+                (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64), np, wbase, wrec, P_<uint32_t>(c->remap),
+                r + pbase);
+        wbase += nw;
+        pbase += np;
+    }
+    HIPCK(hipGetLastError());
+    // (lexid, id0) order: LSD over the id bits, then the word bits
+    int p1 = 0, p2 = 0;
+    c->n_sc = 0;
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false, &p1));
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
+    HIPCK(hipEventRecord(c->ev[3], c->st));
+    c->T = NP;
+    CK(grow(c->uniq, sizeof(uint64_t) * NP));
+    CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
+    uint64_t* ps = P_<uint64_t>(c->pstart);
+    CK(run_scan(c, OpUnique{r, P_<uint64_t>(c->uniq), ps}, NP, ps + c->V));
+    CK(read_u64(c, ps + c->V, &c->U));
+    HIPCK(hipEventRecord(c->ev[4], c->st));
+    c->stats.sort_passes = (uint32_t)(p1 + p2);
+    c->have_pairs = true;
     return II_OK;
 }
 

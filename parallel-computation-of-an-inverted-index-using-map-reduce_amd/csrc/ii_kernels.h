@@ -284,6 +284,25 @@ __global__ __launch_bounds__(kBlock) void k_long_tokens(const uint8_t* __restric
     }
 }
 
+// Next letter (0..25) of a cleaned word at *g, or 26 once the word has ended
+// (whitespace, NUL, end of text, or 299 letters).
+__device__ __forceinline__ uint32_t next_letter(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t* g,
+                                                uint32_t* n) {
+    if (*n >= (uint32_t)kMaxWord) return 26u;
+    while (*g < nbytes) {
+        uint32_t c = text[*g];
+        if (c == 0u || is_ws(c)) break;
+        (*g)++;
+        uint32_t lc = letter_of(c);
+        if (lc < 26u) {
+            (*n)++;
+            return lc;
+        }
+    }
+    *g = nbytes;
+    return 26u;
+}
+
 // Exactness check for hashed keys: every long token must spell the same word
 // as its slot's representative occurrence.
 __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restrict__ text, uint64_t nbytes,
@@ -295,26 +314,15 @@ __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restric
         uint64_t a = lt.pos, b = rep[rec[lt.rec] >> 32];
         if (a == b) continue;
         uint32_t na = 0, nb = 0;
-        bool same = true;
         for (;;) {
-            uint32_t la = 26, lb = 26;
-            while (na < (uint32_t)kMaxWord && a < nbytes) {
-                uint32_t c = text[a];
-                if (c == 0u || is_ws(c)) { a = nbytes; break; }
-                a++;
-                if ((la = letter_of(c)) < 26u) { na++; break; }
+            uint32_t la = next_letter(text, nbytes, &a, &na);
+            uint32_t lb = next_letter(text, nbytes, &b, &nb);
+            if (la != lb) {
+                atomicOr((unsigned long long*)&counters[C_COLLIDE], 1ull);
+                break;
             }
-            while (nb < (uint32_t)kMaxWord && b < nbytes) {
-                uint32_t c = text[b];
-                if (c == 0u || is_ws(c)) { b = nbytes; break; }
-                b++;
-                if ((lb = letter_of(c)) < 26u) { nb++; break; }
-            }
-            if (la != lb || na != nb) { same = false; break; }
-            if (la >= 26u) break;  // both ended
-            if (na == (uint32_t)kMaxWord) break;
+            if (la == 26u) break;
         }
-        if (!same) atomicOr((unsigned long long*)&counters[C_COLLIDE], 1ull);
     }
 }
 
@@ -530,6 +538,19 @@ __device__ __forceinline__ uint32_t ndigits(uint64_t v) {
     return d;
 }
 
+__device__ __forceinline__ void write_word(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t key, uint64_t rep,
+                                           uint32_t len, uint8_t* __restrict__ o) {
+    if ((key & 0xFull) == 0) {
+        for (uint32_t i = 0; i < len; i++) o[i] = (uint8_t)('a' - 1 + ((key >> (59 - 5 * i)) & 31ull));
+    } else {
+        uint32_t n = 0;
+        for (uint64_t g = rep; g < nbytes && n < len; g++) {
+            uint32_t lc = letter_of(text[g]);
+            if (lc < 26u) o[n++] = (uint8_t)('a' + lc);
+        }
+    }
+}
+
 // bytes of one posting: digits of id0+1 plus the following ' ' or ']'
 struct OpPostBytes {
     const uint64_t* uniq;
@@ -561,17 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
     if (j >= V) return;
     uint64_t o = loff[j];
     uint32_t len = lex_len[j];
-    uint64_t k = lex_key[j];
-    if ((k & 0xFull) == 0) {
-        for (uint32_t i = 0; i < len; i++) out[o + i] = (uint8_t)('a' - 1 + ((k >> (59 - 5 * i)) & 31ull));
-    } else {
-        uint32_t n = 0;
-        for (uint64_t g = lex_rep[j]; g < nbytes && n < len; g++) {
-            uint32_t c = text[g];
-            uint32_t lc = letter_of(c);
-            if (lc < 26u) out[o + n++] = (uint8_t)('a' + lc);
-        }
-    }
+    write_word(text, nbytes, lex_key[j], lex_rep[j], len, out + o);
     out[o + len] = ':';
     out[o + len + 1] = '[';
     out[o + len + 3 + (P[post_start[j + 1]] - P[post_start[j]]) - 1] = '\n';
@@ -599,6 +610,73 @@ __global__ void k_letter_off(const uint32_t* __restrict__ letter_start, const ui
     if (l > 26) return;
     uint32_t i = letter_start[l];
     letter_off[l] = i < V ? loff[ord[i]] : total;
+}
+
+// ---------------------------------------------------------------- exchange
+// Segment sent to the owner of a letter range, 8-byte aligned:
+//   u64 header[8] = {kSegMagic, nwords, npairs, arena_bytes, letter_lo, letter_hi, 0, 0}
+//   u64 pairs[npairs]   (word index within the segment) << 32 | id0
+//   u8  arena[]         the segment's words in lexicographic order, each + ' '
+constexpr uint64_t kSegMagic = 0x3147455349495849ull;  // "IXIISEG1"
+
+// word arena offsets: letters + one separator per word
+struct OpWordArena {
+    const uint32_t* llen;
+    uint64_t* woff;
+    __device__ uint64_t value(uint64_t j) const { return (uint64_t)llen[j] + 1; }
+    __device__ void emit(uint64_t j, uint64_t ex, uint64_t) const { woff[j] = ex; }
+};
+
+// per letter l: first word, first pair, first arena byte
+__global__ void k_letter_points(const uint32_t* __restrict__ letter_start, const uint64_t* __restrict__ post_start,
+                                const uint64_t* __restrict__ woff, uint64_t* __restrict__ pts) {
+    int l = threadIdx.x;
+    if (l > 26) return;
+    uint32_t j = letter_start[l];
+    pts[3 * l] = j;
+    pts[3 * l + 1] = post_start[j];
+    pts[3 * l + 2] = woff[j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_export_words(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                         const uint64_t* __restrict__ lex_key,
+                                                         const uint64_t* __restrict__ lex_rep,
+                                                         const uint32_t* __restrict__ lex_len,
+                                                         const uint64_t* __restrict__ woff, uint32_t j0, uint32_t j1,
+                                                         uint8_t* __restrict__ arena) {
+    uint32_t j = j0 + blockIdx.x * kBlock + threadIdx.x;
+    if (j >= j1) return;
+    uint8_t* o = arena + (woff[j] - woff[j0]);
+    uint32_t len = lex_len[j];
+    write_word(text, nbytes, lex_key[j], lex_rep[j], len, o);
+    o[len] = ' ';
+}
+
+__global__ __launch_bounds__(kBlock) void k_export_pairs(const uint64_t* __restrict__ uniq, uint64_t p0, uint64_t p1,
+                                                         uint32_t j0, uint64_t* __restrict__ out) {
+    for (uint64_t p = p0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < p1; p += (uint64_t)gridDim.x * kBlock) {
+        uint64_t r = uniq[p];
+        out[p - p0] = (((r >> 32) - j0) << 32) | (r & 0xFFFFFFFFull);
+    }
+}
+
+__global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint64_t npairs, uint64_t arena, uint64_t llo,
+                                uint64_t lhi) {
+    if (threadIdx.x == 0) {
+        h[0] = kSegMagic; h[1] = nwords; h[2] = npairs; h[3] = arena; h[4] = llo; h[5] = lhi; h[6] = 0; h[7] = 0;
+    }
+}
+
+// received pair -> (global lexid, id0): word k of the merged word text was
+// tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id
+__global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restrict__ pairs, uint64_t np, uint64_t wbase,
+                                                         const uint64_t* __restrict__ wrec,
+                                                         const uint32_t* __restrict__ remap, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
+        uint64_t r = pairs[i];
+        uint64_t slot = wrec[wbase + (r >> 32)] >> 32;
+        out[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
+    }
 }
 
 }  // namespace ii

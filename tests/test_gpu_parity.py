@@ -156,3 +156,52 @@ def test_zipf_medium_vs_oracle(idx):
     idx.map_host(t, off.tolist(), ids)
     idx.reduce()
     assert_same(idx.letters(), oracle_index(t, off, ids), "zipf48M")
+
+
+# ---------------------------------------------------------------- multi-GPU exchange logic
+def shard_and_merge(text, off, G, id_bound=None):
+    """G logical shards on one device: files split by the reference's size
+    heuristic (ii_partition), each shard mapped in its own context, letter
+    ranges exchanged (ii_export / ii_import) and formatted by their owner."""
+    import ii_dist
+    n = len(off) - 1
+    sizes = [off[i + 1] - off[i] for i in range(n)]
+    order, sb, se = ii_ctypes.partition(sizes, G)
+    idxs = []
+    for g in range(G):
+        fids = sorted(order[sb[g]:se[g]])
+        t = bytearray()
+        o = [0]
+        for f in fids:
+            t += text[off[f]:off[f + 1]]
+            o.append(len(t))
+        ix = ii_ctypes.Index(0)
+        ix.map_host(bytes(t), o, fids)
+        idxs.append(ix)
+    ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else n)
+    merged = {}
+    for g, ix in enumerate(idxs):
+        lo, hi = ii_ctypes.reducer_letters(g, G)
+        got = ix.letters()
+        for l in range(26):
+            ch = chr(97 + l)
+            if lo <= l < hi:
+                merged[ch] = got[ch]
+            else:
+                assert got[ch] == b"", "rank %d holds letter %s it does not own" % (g, ch)
+        ix.close()
+    return merged
+
+
+@pytest.mark.parametrize("case,G", [("config2", 2), ("config2", 3), ("zipf_small", 4), ("edge", 5), ("rand_1", 8),
+                                    ("tiny360", 2)])
+def test_logical_shards_match_reference(case, G):
+    text, off, ids, expected = case_arrays(case)
+    assert_same(shard_and_merge(text, off, G), expected, "%s G=%d" % (case, G))
+
+
+def test_logical_shards_zipf_vs_oracle():
+    t, off = ii_ctypes.zipf_corpus(24_000_000, 300, 200_000, 33, threads=8)
+    off = off.tolist()
+    text = t.tobytes()
+    assert_same(shard_and_merge(text, off, 4), oracle_index(text, off, list(range(300))), "zipf G=4")
