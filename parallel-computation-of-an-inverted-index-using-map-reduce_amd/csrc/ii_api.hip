@@ -40,7 +40,7 @@ struct ii_ctx {
     DBuf fstart, fid;
 
     // scratch
-    DBuf partial, totals, counters, chunk_cnt, rtable;
+    DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable;
     // K1
     DBuf rec, rec2, longs;
     DBuf tkeys, trep;
@@ -134,6 +134,23 @@ static int run_scan(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
     return II_OK;
 }
 
+// Sum of op.value over [0, n) -> *d_total (reduce + partials only).
+template <class Op>
+static int run_reduce(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
+    if (n == 0) {
+        HIPCK(hipMemsetAsync(d_total, 0, sizeof(uint64_t), c->st));
+        return II_OK;
+    }
+    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kBlock - 1) / kBlock);
+    uint64_t chunk = ((n + nch - 1) / nch + kBlock - 1) / kBlock * kBlock;
+    nch = (n + chunk - 1) / chunk;
+    uint64_t* part = P_<uint64_t>(c->partial);
+    k_scan_reduce<Op><<<(uint32_t)nch, kBlock, 0, c->st>>>(op, n, chunk, part);
+    k_scan_partials<<<1, kBlock, 0, c->st>>>(part, (uint32_t)nch, d_total);
+    HIPCK(hipGetLastError());
+    return II_OK;
+}
+
 struct OpInPlace {
     uint64_t* a;
     __device__ uint64_t value(uint64_t i) const { return a[i]; }
@@ -143,7 +160,7 @@ struct OpInPlace {
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
-                    bool timed, int* passes) {
+                    bool timed, int* passes, const uint32_t* remap0 = nullptr) {
     if (passes) *passes = 0;
     if (n <= 1 || hi <= lo) return II_OK;
     uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
@@ -153,15 +170,17 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     uint64_t* table = P_<uint64_t>(c->rtable);
     const bool kv = v != nullptr;
     for (int shift = lo; shift < hi; shift += kRadixBits) {
-        k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table);
+        const uint32_t* remap = shift == lo ? remap0 : nullptr;
+        k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
         CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
         if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
         if (kv)
-            k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift, (uint32_t)nch, table);
+            k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift, (uint32_t)nch, table,
+                                                                       remap);
         else
             k_radix_scatter<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
-                                                                        (uint32_t)nch, table);
+                                                                        (uint32_t)nch, table, remap);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
             c->n_sc++;
@@ -212,7 +231,7 @@ extern "C" void ii_close(ii_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DBuf* all[] = {&c->text_own, &c->fstart, &c->fid,   &c->partial, &c->totals, &c->counters, &c->chunk_cnt,
+    DBuf* all[] = {&c->text_own, &c->fstart, &c->fid,   &c->partial, &c->totals, &c->counters, &c->chunk_cnt, &c->chunk_hist,
                    &c->rtable,   &c->rec,    &c->rec2,  &c->longs,   &c->tkeys,  &c->trep,     &c->dslot,
                    &c->dkey,     &c->dkey2,  &c->didx,  &c->didx2,   &c->remap,  &c->lkey,     &c->lrep,
                    &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
@@ -267,14 +286,13 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
     }
     const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
     CK(grow(c->chunk_cnt, sizeof(uint64_t) * nch));
+    CK(grow(c->chunk_hist, sizeof(uint32_t) * 26 * nch));
     uint64_t* chunk_cnt = P_<uint64_t>(c->chunk_cnt);
     const uint64_t* fstart = P_<uint64_t>(c->fstart);
     const uint32_t* fid = P_<uint32_t>(c->fid);
 
     k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, counters);
-    Table dummy{nullptr, nullptr, 0, 0, counters};
-    k_tokenize<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, dummy,
-                                                          nullptr, nullptr, 0);
+    k_tok_count<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, chunk_cnt);
     CK(run_scan(c, OpInPlace{chunk_cnt}, nch, totals));
     uint64_t hv[2];
     CK(read_u64(c, totals, &hv[0]));
@@ -287,15 +305,18 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
 
     for (int attempt = 0;; attempt++) {
         if (attempt > 12) return II_ERR_INTERNAL;
+        if (c->table_cap > (1ull << 31)) return II_ERR_NOMEM;  // slots must fit 31 bits
         CK(grow(c->tkeys, sizeof(uint64_t) * c->table_cap));
         CK(grow(c->trep, sizeof(uint64_t) * c->table_cap));
         CK(grow(c->longs, sizeof(LongTok) * c->long_cap));
         HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * c->table_cap, c->st));
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->table_cap - 1, c->seed, counters};
-        k_tokenize<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
-                                                             P_<uint64_t>(c->rec), P_<LongTok>(c->longs), c->long_cap);
+        k_tok_emit<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
+                                                       P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
+                                                       P_<LongTok>(c->longs), c->long_cap);
         HIPCK(hipGetLastError());
+        CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, c->table_cap, counters + C_INSERT));
         uint64_t cnt[4];
         CK(read_u64(c, counters, cnt, 4));
         if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] * 2 > c->table_cap) {
@@ -311,17 +332,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         c->nlong = cnt[C_LONG];
         if (c->nlong) {
             uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(c->nlong));
-            k_long_tokens<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong, tab,
-                                                 P_<uint64_t>(c->rec));
-            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong, P_<uint64_t>(c->rec),
+            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong,
                                                  P_<uint64_t>(c->trep), counters);
             HIPCK(hipGetLastError());
             CK(read_u64(c, counters, cnt, 4));
-            if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] * 2 > c->table_cap) {
-                c->table_cap *= 4;
-                c->retries++;
-                continue;
-            }
             if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
                 c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
                 c->retries++;
@@ -331,6 +345,8 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         c->V = cnt[C_INSERT];
         break;
     }
+    k_hist_reduce<<<26, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
+    HIPCK(hipGetLastError());
     CK(read_u64(c, counters + C_HIST, c->hist, II_ALPHABET));
     if (hist_out) memcpy(hist_out, c->hist, sizeof(c->hist));
     HIPCK(hipEventRecord(c->ev[1], c->st));
@@ -555,10 +571,12 @@ static int local_reduce(ii_ctx* c) {
     // ---- K2: sort records by (lexid, fid); fid order is kept by stability
     uint64_t* r = P_<uint64_t>(c->rec);
     uint64_t* r2 = P_<uint64_t>(c->rec2);
-    k_remap<<<(uint32_t)std::min<uint64_t>(16384, grid_for(T)), kBlock, 0, c->st>>>(r, T, P_<uint32_t>(c->remap));
-    HIPCK(hipGetLastError());
     const int lb = std::max(1, bitlen(V - 1));
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes));
+    if (T == 1) {  // nothing to sort: remap in place
+        k_remap<<<1, kBlock, 0, c->st>>>(r, T, P_<uint32_t>(c->remap));
+        HIPCK(hipGetLastError());
+    }
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap)));
     c->rec_sorted = r;
     HIPCK(hipEventRecord(c->ev[3], c->st));
 

@@ -1,8 +1,8 @@
 // ii_kernels.h — the inverted-index kernels (K1..K5) for MI355X (gfx950).
 //
 // Reference path replaced (see DESIGN.md for the full map):
-//   K1 k_tokenize      mapper() hot loop, main.c:102-118, + partial files main.c:116
-//   K1 k_long_tokens   same, for words longer than 12 letters
+//   K1 k_tok_count/k_tok_emit  mapper() hot loop, main.c:102-118, + partial
+//                      files main.c:116 (records, word table, letter counts)
 //   Kd dictionary      (no reference equivalent: gives every distinct word a
 //                      lexicographic id so that the reducer's strcmp order,
 //                      main.c:63, becomes integer order)
@@ -25,24 +25,17 @@ constexpr int kMaxWord = 299;      // MAX_WORD - 1 letters (main.c:7, 105)
 constexpr int kMaxProbe = 1 << 14;
 
 constexpr uint32_t kSlotNone = 0xFFFFFFFFu;  // token with no letters (dropped, main.c:113)
-constexpr uint32_t kSlotLong = 0xFFFFFFFEu;  // > 12 letters: finished by k_long_tokens
 
 // counters[] layout (u64)
 enum : int {
     C_LONG = 0,      // long tokens appended
     C_OVERFLOW = 1,  // word table probe limit hit / long list full
-    C_INSERT = 2,    // distinct keys inserted
+    C_INSERT = 2,    // distinct keys (set from a scan of the table)
     C_COLLIDE = 3,   // long-word hash collision detected
     C_HIST = 4,      // 26 first-letter counters
     C_TIES = 30,     // dictionary entries sharing a 12-letter prefix
     C_MAXLEN = 31,   // longest tied word
     C_NUM = 32
-};
-
-struct LongTok {
-    uint64_t pos;   // token start in text
-    uint64_t rec;   // record index
-    uint64_t fid;   // file id (u32)
 };
 
 // C-locale isspace: the fscanf("%s") delimiter set (main.c:102).
@@ -77,9 +70,8 @@ __device__ __forceinline__ uint32_t table_insert(const Table& t, uint64_t key, u
         if (k == key) return (uint32_t)h;
         if (k == 0ull) {
             unsigned long long old = atomicCAS(&t.keys[h], 0ull, (unsigned long long)key);
-            if (old == 0ull) {
+            if (old == 0ull) {  // inserted; distinct words are counted later by a scan of the table
                 t.rep[h] = pos;
-                atomicAdd((unsigned long long*)&t.counters[C_INSERT], 1ull);
                 return (uint32_t)h;
             }
             if (old == key) return (uint32_t)h;
@@ -91,161 +83,6 @@ __device__ __forceinline__ uint32_t table_insert(const Table& t, uint64_t key, u
 }
 
 // ---------------------------------------------------------------- K1 tokenizer
-struct Walk {
-    uint64_t packed;  // first 12 letter codes (1..26), left aligned
-    uint32_t nlet;    // letters seen, stops counting at 13
-    uint32_t first;   // first letter index
-};
-
-// Walk a token from tile-local byte p: cleaning loop of main.c:105-111 (stops at
-// NUL, whitespace, or once a 13th letter shows the word is "long").
-__device__ __forceinline__ Walk walk_token(const uint8_t* s, const uint8_t* __restrict__ text, uint64_t nbytes,
-                                           uint64_t tile_lo, uint32_t p) {
-    Walk w{0ull, 0u, 0u};
-    for (uint32_t j = p;; j++) {
-        uint32_t c;
-        if (j < (uint32_t)(kTile + kHalo)) c = s[16 + j];
-        else {
-            uint64_t g = tile_lo + j;
-            c = g < nbytes ? text[g] : 32u;
-        }
-        if (c == 0u || is_ws(c)) break;
-        uint32_t lc = letter_of(c);
-        if (lc < 26u) {
-            if (w.nlet == 0) w.first = lc;
-            w.nlet++;
-            if (w.nlet > 12) break;
-            w.packed |= (uint64_t)(lc + 1) << (64 - 5 * w.nlet);
-        }
-    }
-    return w;
-}
-
-// file index of byte position pos: last f in [f_lo, f_hi] with start[f] <= pos
-__device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ start, uint32_t f_lo, uint32_t f_hi, uint64_t pos) {
-    while (f_lo < f_hi) {
-        uint32_t mid = f_lo + (f_hi - f_lo + 1) / 2;
-        if (start[mid] <= pos) f_lo = mid;
-        else f_hi = mid - 1;
-    }
-    return f_lo;
-}
-
-// kEmit = false: count kept tokens per chunk -> chunk_cnt[blockIdx.x].
-// kEmit = true : chunk_cnt holds exclusive offsets; write records
-//                rec[i] = slot << 32 | fid in text order, insert words into the
-//                table, count first letters, and queue long tokens.
-template <bool kEmit>
-__global__ __launch_bounds__(kBlock) void k_tokenize(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                     const uint64_t* __restrict__ file_start,
-                                                     const uint32_t* __restrict__ file_id, uint32_t nfiles,
-                                                     uint64_t* __restrict__ chunk_cnt, Table tab,
-                                                     uint64_t* __restrict__ rec, LongTok* __restrict__ longs,
-                                                     uint64_t long_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
-    __shared__ uint32_t s_slot[kEmit ? kTile : 1];
-    __shared__ uint64_t s_scan[kWaves + 1];
-    __shared__ uint32_t s_hist[32];
-    __shared__ uint32_t s_f[2];
-
-    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
-    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
-    const int t = threadIdx.x;
-    if (t < 32) s_hist[t] = 0;
-    if (kEmit && t == 0) {
-        s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
-        s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
-    }
-    uint64_t out = kEmit ? chunk_cnt[blockIdx.x] : 0;
-    uint64_t kept_all = 0;
-
-    for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
-        __syncthreads();
-        // stage [tile_lo - 16, tile_lo + kTile + kHalo) in 16-byte pieces; bytes
-        // outside the text read as ' ' (so position 0 starts a token).
-        for (int q = t; q < (16 + kTile + kHalo) / 16; q += kBlock) {
-            const int64_t g = (int64_t)tile_lo - 16 + (int64_t)q * 16;
-            uint4 v;
-            if (g >= 0 && (uint64_t)g + 16 <= nbytes) {
-                v = *reinterpret_cast<const uint4*>(text + g);
-            } else {
-                uint8_t b[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    int64_t gi = g + i;
-                    b[i] = (gi >= 0 && (uint64_t)gi < nbytes) ? text[gi] : (uint8_t)32;
-                }
-                v = *reinterpret_cast<uint4*>(b);
-            }
-            *reinterpret_cast<uint4*>(s_text + q * 16) = v;
-        }
-        __syncthreads();
-
-        const uint32_t wlo = (uint32_t)t * 16;
-        // token starts in this lane's 16 bytes: non-space after space (main.c:102)
-        uint32_t starts = 0;
-        {
-            uint32_t prev = s_text[16 + wlo - 1];
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                uint32_t c = s_text[16 + wlo + i];
-                if (!is_ws(c) && is_ws(prev)) starts |= 1u << i;
-                prev = c;
-            }
-        }
-        uint32_t kept = 0;
-        for (uint32_t m = starts; m; m &= m - 1) {
-            const uint32_t i = __builtin_ctz(m);
-            Walk w = walk_token(s_text, text, nbytes, tile_lo, wlo + i);
-            if (w.nlet == 0) {
-                if (kEmit) s_slot[wlo + i] = kSlotNone;
-                continue;
-            }
-            kept++;
-            if (kEmit) {
-                atomicAdd(&s_hist[w.first], 1u);
-                s_slot[wlo + i] = w.nlet <= 12 ? table_insert(tab, w.packed, tile_lo + wlo + i) : kSlotLong;
-            }
-        }
-        if (!kEmit) {
-            kept_all += kept;
-            continue;
-        }
-        uint64_t tot;
-        uint64_t o = out + block_excl_scan(kept, &tot, s_scan);
-        out += tot;
-        if (kept) {
-            const uint64_t gpos = tile_lo + wlo;
-            uint32_t f = file_of(file_start, s_f[0], s_f[1], gpos);
-            for (uint32_t m = starts; m; m &= m - 1) {
-                const uint32_t i = __builtin_ctz(m);
-                const uint32_t slot = s_slot[wlo + i];
-                if (slot == kSlotNone) continue;
-                const uint64_t pos = gpos + i;
-                while (f < s_f[1] && file_start[f + 1] <= pos) f++;
-                const uint32_t fid = file_id[f];
-                if (slot == kSlotLong) {
-                    uint64_t li = atomicAdd((unsigned long long*)&tab.counters[C_LONG], 1ull);
-                    if (li < long_cap) longs[li] = LongTok{pos, o, fid};
-                    else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-                    rec[o] = fid;
-                } else {
-                    rec[o] = ((uint64_t)slot << 32) | fid;
-                }
-                o++;
-            }
-        }
-    }
-    if (!kEmit) {
-        uint64_t tot;
-        (void)block_excl_scan(kept_all, &tot, s_scan);
-        if (t == 0) chunk_cnt[blockIdx.x] = tot;
-    } else {
-        __syncthreads();
-        if (t < 26 && s_hist[t]) atomicAdd((unsigned long long*)&tab.counters[C_HIST + t], (unsigned long long)s_hist[t]);
-    }
-}
-
 // Full cleaned word at a token start (main.c:105-111, <= 299 letters):
 // length, FNV-style hash of the letter codes and the first-12 prefix.
 struct LongWord {
@@ -269,20 +106,377 @@ __device__ __forceinline__ LongWord read_word(const uint8_t* __restrict__ text, 
     return w;
 }
 
-__device__ __forceinline__ uint64_t long_key(const LongWord& w, uint64_t seed) {
-    return (mix64(w.hash ^ seed ^ ((uint64_t)w.len << 48)) << 4) | 0xFull;
+__device__ __forceinline__ uint64_t long_key(uint64_t hash, uint32_t len, uint64_t seed) {
+    return (mix64(hash ^ seed ^ ((uint64_t)len << 48)) << 4) | 0xFull;
 }
 
-__global__ __launch_bounds__(kBlock) void k_long_tokens(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                        const LongTok* __restrict__ longs, uint64_t nlong, Table tab,
-                                                        uint64_t* __restrict__ rec) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nlong; i += (uint64_t)gridDim.x * kBlock) {
-        LongTok lt = longs[i];
-        LongWord w = read_word(text, nbytes, lt.pos);
-        uint32_t slot = table_insert(tab, long_key(w, tab.seed), lt.pos);
-        rec[lt.rec] = ((uint64_t)slot << 32) | lt.fid;
+// Reader of the staged tile: tile-local byte j (j >= -16); LDS is read one
+// aligned dword at a time (the walk touches ~2 dwords per token instead of
+// ~7 bytes), past the halo it falls back to global memory.
+struct TileReader {
+    const uint8_t* s;
+    const uint8_t* __restrict__ text;
+    uint64_t nbytes, tile_lo;
+    uint32_t di, dw;
+    __device__ __forceinline__ TileReader(const uint8_t* s_, const uint8_t* text_, uint64_t nb, uint64_t lo)
+        : s(s_), text(text_), nbytes(nb), tile_lo(lo), di(0xFFFFFFFFu), dw(0) {}
+    __device__ __forceinline__ uint32_t get(uint32_t j) {
+        if (j < (uint32_t)(kTile + kHalo)) {
+            const uint32_t a = 16 + j;
+            if ((a >> 2) != di) {
+                di = a >> 2;
+                dw = reinterpret_cast<const uint32_t*>(s)[di];
+            }
+            return (dw >> ((a & 3) * 8)) & 0xFFu;
+        }
+        const uint64_t g = tile_lo + j;
+        return g < nbytes ? text[g] : 32u;
+    }
+};
+
+// Cleaning loop of main.c:105-111 from tile-local byte p: stops at whitespace,
+// NUL or the 299th letter.  Returns the word key (exact 5-bit packing for
+// <= 12 letters, tagged hash otherwise) and its letter count (0 = dropped).
+struct TokKey {
+    uint64_t key;
+    uint32_t nlet;
+    uint32_t first;
+};
+__device__ __forceinline__ TokKey token_key(TileReader& rd, uint32_t p, uint64_t seed) {
+    uint64_t packed = 0, hash = 1469598103934665603ull;
+    uint32_t n = 0, first = 0;
+    for (uint32_t j = p;; j++) {
+        const uint32_t c = rd.get(j);
+        if (c == 0u || is_ws(c)) break;
+        const uint32_t lc = letter_of(c);
+        if (lc < 26u) {
+            if (n == 0) first = lc;
+            n++;
+            if (n <= 12) packed |= (uint64_t)(lc + 1) << (64 - 5 * n);
+            hash = (hash ^ (lc + 1)) * 1099511628211ull;
+            if (n == (uint32_t)kMaxWord) break;
+        }
+    }
+    return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
+}
+
+// A token is kept iff a letter comes before the first whitespace / NUL
+// (main.c:105, 113).  Cheap form for the count pass.
+__device__ __forceinline__ bool token_kept(TileReader& rd, uint32_t p) {
+    for (uint32_t j = p;; j++) {
+        const uint32_t c = rd.get(j);
+        if (c == 0u || is_ws(c)) return false;
+        if (letter_of(c) < 26u) return true;
     }
 }
+
+// file index of byte position pos: last f in [f_lo, f_hi] with start[f] <= pos
+__device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ start, uint32_t f_lo, uint32_t f_hi, uint64_t pos) {
+    while (f_lo < f_hi) {
+        uint32_t mid = f_lo + (f_hi - f_lo + 1) / 2;
+        if (start[mid] <= pos) f_lo = mid;
+        else f_hi = mid - 1;
+    }
+    return f_lo;
+}
+
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, uint64_t nbytes, int64_t g) {
+    if (g >= 0 && (uint64_t)g + 16 <= nbytes) return *reinterpret_cast<const uint4*>(text + g);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int64_t gi = g + i;
+        const uint32_t b = (gi >= 0 && (uint64_t)gi < nbytes) ? text[gi] : 32u;
+        w[i >> 2] |= b << ((i & 3) * 8);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Stage text [tile_lo - 16, tile_lo + kTile + kHalo) into LDS with 16-B
+// loads; lane t's own window [tile_lo + 16t, +16) is returned in registers.
+// Bytes outside the text read as ' ' (so position 0 starts a token).
+__device__ __forceinline__ uint4 stage_tile(uint8_t* s_text, const uint8_t* __restrict__ text, uint64_t nbytes,
+                                            uint64_t tile_lo) {
+    const int t = threadIdx.x;
+    const uint4 v = load16(text, nbytes, (int64_t)tile_lo + 16 * t);
+    *reinterpret_cast<uint4*>(s_text + 16 + 16 * t) = v;
+    constexpr int kExtra = 1 + kHalo / 16;  // left piece + halo pieces
+    if (t < kExtra) {
+        const int q = t == 0 ? -1 : kTile / 16 + t - 1;
+        *reinterpret_cast<uint4*>(s_text + 16 + 16 * q) = load16(text, nbytes, (int64_t)tile_lo + 16 * q);
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {
+    const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
+    return (w >> ((i & 3) * 8)) & 0xFFu;
+}
+
+// ---- SWAR byte classes, 4 bytes per u32 (exact, no inter-byte carries)
+// bit 7 of each byte set where the byte is zero
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+// the four bit-7 flags -> a 4-bit mask
+__device__ __forceinline__ uint32_t hb4(uint32_t m) {
+    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+struct Classes {
+    uint32_t ws, letter, nul;  // 16-bit masks over the lane's window
+};
+__device__ __forceinline__ void classify4(uint32_t x, uint32_t& ws, uint32_t& let, uint32_t& nul) {
+    const uint32_t hb = x & 0x80808080u;
+    const uint32_t y = x & 0x7F7F7F7Fu;
+    const uint32_t sp = zero_bytes(x ^ 0x20202020u);                                  // ' '
+    const uint32_t ctl = (y + 0x77777777u) & ~(y + 0x72727272u) & ~hb & 0x80808080u;   // 9..13
+    ws = hb4(sp | ctl);                                   // C-locale isspace (main.c:102)
+    const uint32_t z = (x | 0x20202020u) & 0x7F7F7F7Fu;
+    let = hb4((z + 0x1F1F1F1Fu) & ~(z + 0x05050505u) & ~hb & 0x80808080u);  // A-Z / a-z (main.c:106-110)
+    nul = hb4(zero_bytes(x));
+}
+__device__ __forceinline__ Classes classify16(const uint4& v) {
+    Classes c{0, 0, 0};
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t a, b, n;
+        classify4(w[k], a, b, n);
+        c.ws |= a << (4 * k);
+        c.letter |= b << (4 * k);
+        c.nul |= n << (4 * k);
+    }
+    return c;
+}
+
+// Token starts of the lane's window (non-space after space, main.c:102).  The
+// byte before the window comes from the neighbour lane (LDS for lane 0 of a
+// wave).  Call after the staging barrier.
+__device__ __forceinline__ uint32_t lane_starts(const uint4& v, const Classes& cl, const uint8_t* s_text) {
+    const int t = threadIdx.x;
+    uint32_t prev = __shfl_up(v.w, 1, 64) >> 24;
+    if ((t & 63) == 0) prev = s_text[16 + 16 * t - 1];
+    const uint32_t prev_ws = is_ws(prev) ? 1u : 0u;
+    return ~cl.ws & ((cl.ws << 1) | prev_ws) & 0xFFFFu;
+}
+
+// Kept tokens among the starts (a letter before the first whitespace / NUL,
+// main.c:105, 113); decided from the masks, walking LDS only when the window
+// ends before the token shows a letter, space or NUL.
+__device__ __forceinline__ uint32_t kept_starts(uint32_t starts, const Classes& cl, const uint8_t* s_text,
+                                                const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t tile_lo,
+                                                uint32_t wlo) {
+    const uint32_t ev = cl.letter | cl.ws | cl.nul;
+    uint32_t kept = 0;
+    for (uint32_t m = starts & ~cl.letter; m; m &= m - 1) {  // starts that are not letters themselves
+        const uint32_t i = __builtin_ctz(m);
+        const uint32_t e = ev >> i;
+        bool k;
+        if (e) k = (cl.letter >> (i + __builtin_ctz(e))) & 1u;
+        else {
+            TileReader rd(s_text, text, nbytes, tile_lo);
+            k = token_kept(rd, wlo + 16);
+        }
+        kept |= (uint32_t)k << i;
+    }
+    return kept | (starts & cl.letter);
+}
+
+// K1a: kept tokens per 64 KiB chunk -> chunk_cnt[blockIdx.x].
+__global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                      uint64_t* __restrict__ chunk_cnt) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
+    __shared__ uint64_t s_scan[kWaves + 1];
+    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
+    const uint32_t wlo = (uint32_t)threadIdx.x * 16;
+    uint64_t kept = 0;
+    for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
+        __syncthreads();
+        const uint4 v = stage_tile(s_text, text, nbytes, tile_lo);
+        __syncthreads();
+        const Classes cl = classify16(v);
+        kept += __popc(kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo));
+    }
+    uint64_t tot;
+    (void)block_excl_scan(kept, &tot, s_scan);
+    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = tot;
+}
+
+// Long token queued for the exactness check (k_long_verify).
+struct LongTok {
+    uint64_t pos;   // token start
+    uint64_t slot;  // word-table slot it was given
+};
+constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
+
+// Probe / insert starting from home slot h with the key at slot h already read.
+__device__ __forceinline__ uint32_t table_resolve(const Table& t, uint64_t key, uint64_t h, unsigned long long k,
+                                                  uint64_t pos) {
+    for (int probe = 0; probe < kMaxProbe; probe++) {
+        if (k == key) return (uint32_t)h;
+        if (k == 0ull) {
+            unsigned long long old = atomicCAS(&t.keys[h], 0ull, (unsigned long long)key);
+            if (old == 0ull) {
+                t.rep[h] = pos;
+                return (uint32_t)h;
+            }
+            if (old == key) return (uint32_t)h;
+        }
+        h = (h + 1) & t.mask;
+        k = t.keys[h];
+    }
+    atomicOr((unsigned long long*)&t.counters[C_OVERFLOW], 1ull);
+    return 0;
+}
+
+// K1b: chunk_off holds exclusive record offsets.  Per 4 KiB tile:
+//   1. masks -> kept token starts, block scan -> token index per lane
+//   2. each lane walks its kept tokens (LDS) -> word key into s_key[index]
+//   3. the tile's tokens are spread evenly over the 256 threads, which probe
+//      the word table with up to 4 independent loads in flight each
+//   4. records rec[i] = slot << 32 | file id0 leave through LDS, coalesced.
+// First letters are counted per chunk (chunk_hist[chunk][26] = the
+// partial_<letter>.txt line counts); tokens of > 12 letters are queued for the
+// hash-collision check.  No global atomics on a shared word per token.
+__global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                     const uint64_t* __restrict__ file_start,
+                                                     const uint32_t* __restrict__ file_id, uint32_t nfiles,
+                                                     const uint64_t* __restrict__ chunk_off, Table tab,
+                                                     uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
+                                                     LongTok* __restrict__ longs, uint64_t long_cap) {
+    constexpr int kMaxTok = kTile / 2 + 1;
+    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
+    __shared__ uint64_t s_key[kMaxTok];   // word key, then the record
+    __shared__ uint16_t s_off[kMaxTok];   // tile offset | 0x8000 if long
+    __shared__ LongTok s_long[kLongBuf];
+    __shared__ uint64_t s_scan[kWaves + 1];
+    __shared__ uint32_t s_hist[32];
+    __shared__ uint32_t s_f[2];
+    __shared__ uint32_t s_lcount;
+    __shared__ uint64_t s_lbase;
+
+    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
+    const int t = threadIdx.x;
+    if (t < 32) s_hist[t] = 0;
+    if (t == 0) {
+        s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
+        s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
+        s_lcount = 0;
+    }
+    uint64_t out = chunk_off[blockIdx.x];
+    const uint32_t wlo = (uint32_t)t * 16;
+
+    for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
+        __syncthreads();
+        const uint4 v = stage_tile(s_text, text, nbytes, tile_lo);
+        __syncthreads();
+        // 1. kept starts
+        const Classes cl = classify16(v);
+        const uint32_t kept = kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo);
+        uint64_t tot;
+        uint32_t o = (uint32_t)block_excl_scan(__popc(kept), &tot, s_scan);
+        // 2. walk
+        uint32_t nlong = 0;
+        {
+            TileReader rd(s_text, text, nbytes, tile_lo);
+            for (uint32_t m = kept; m; m &= m - 1) {
+                const uint32_t i = __builtin_ctz(m);
+                const TokKey k = token_key(rd, wlo + i, tab.seed);
+                atomicAdd(&s_hist[k.first], 1u);
+                s_key[o] = k.key;
+                s_off[o] = (uint16_t)((wlo + i) | (k.nlet > 12 ? 0x8000u : 0u));
+                nlong += k.nlet > 12;
+                o++;
+            }
+        }
+        uint64_t ltot;
+        (void)block_excl_scan(nlong, &ltot, s_scan);  // also the barrier before phase 3
+        // long-token queue: LDS buffer, one global atomic per flush
+        const bool direct = ltot > (uint64_t)kLongBuf;
+        if (ltot && (direct || s_lcount + ltot > (uint64_t)kLongBuf)) {
+            if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)s_lcount);
+            __syncthreads();
+            for (uint32_t q = t; q < s_lcount; q += kBlock) {
+                if (s_lbase + q < long_cap) longs[s_lbase + q] = s_long[q];
+                else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+            }
+            __syncthreads();
+            if (t == 0) {
+                s_lcount = 0;
+                if (direct) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)ltot);
+            }
+            __syncthreads();
+        }
+        // 3. probe: token q = t + u*kBlock, four loads in flight per thread
+        const uint32_t ntok = (uint32_t)tot;
+        for (uint32_t base = t; base < ntok; base += 4 * kBlock) {
+            uint64_t key[4], h[4];
+            unsigned long long kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t q = base + u * kBlock;
+                key[u] = q < ntok ? s_key[q] : 0ull;
+                h[u] = mix64(key[u] ^ tab.seed) & tab.mask;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) kk[u] = (base + u * kBlock < ntok) ? tab.keys[h[u]] : 0ull;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t q = base + u * kBlock;
+                if (q >= ntok) continue;
+                const uint32_t off = s_off[q];
+                const uint64_t pos = tile_lo + (off & 0x7FFFu);
+                const uint32_t slot = kk[u] == key[u] ? (uint32_t)h[u] : table_resolve(tab, key[u], h[u], kk[u], pos);
+                const uint32_t f = s_f[0] == s_f[1] ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
+                s_key[q] = ((uint64_t)slot << 32) | file_id[f];
+                if (off & 0x8000u) {
+                    if (direct) {
+                        const uint64_t li = s_lbase + atomicAdd(&s_lcount, 1u);
+                        if (li < long_cap) longs[li] = LongTok{pos, slot};
+                        else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+                    } else {
+                        s_long[atomicAdd(&s_lcount, 1u)] = LongTok{pos, slot};
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (direct && t == 0) s_lcount = 0;
+        // 4. coalesced record store
+        for (uint32_t q = t; q < ntok; q += kBlock) rec[out + q] = s_key[q];
+        out += tot;
+    }
+    __syncthreads();
+    if (s_lcount) {
+        if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)s_lcount);
+        __syncthreads();
+        for (uint32_t q = t; q < s_lcount; q += kBlock) {
+            if (s_lbase + q < long_cap) longs[s_lbase + q] = s_long[q];
+            else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+        }
+    }
+    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
+}
+
+// counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
+__global__ __launch_bounds__(kBlock) void k_hist_reduce(const uint32_t* __restrict__ chunk_hist, uint64_t nch,
+                                                        uint64_t* __restrict__ counters) {
+    __shared__ uint64_t s_scan[kWaves + 1];
+    uint64_t acc = 0;
+    for (uint64_t c = threadIdx.x; c < nch; c += kBlock) acc += chunk_hist[c * 26 + blockIdx.x];
+    uint64_t tot;
+    (void)block_excl_scan(acc, &tot, s_scan);
+    if (threadIdx.x == 0) counters[C_HIST + blockIdx.x] = tot;
+}
+
+// number of occupied word-table slots
+struct OpOccupied {
+    const unsigned long long* keys;
+    __device__ uint64_t value(uint64_t i) const { return keys[i] != 0ull; }
+    __device__ void emit(uint64_t, uint64_t, uint64_t) const {}
+};
 
 // Next letter (0..25) of a cleaned word at *g, or 26 once the word has ended
 // (whitespace, NUL, end of text, or 299 letters).
@@ -307,11 +501,10 @@ __device__ __forceinline__ uint32_t next_letter(const uint8_t* __restrict__ text
 // as its slot's representative occurrence.
 __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         const LongTok* __restrict__ longs, uint64_t nlong,
-                                                        const uint64_t* __restrict__ rec, const uint64_t* __restrict__ rep,
-                                                        uint64_t* counters) {
+                                                        const uint64_t* __restrict__ rep, uint64_t* counters) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nlong; i += (uint64_t)gridDim.x * kBlock) {
         LongTok lt = longs[i];
-        uint64_t a = lt.pos, b = rep[rec[lt.rec] >> 32];
+        uint64_t a = lt.pos, b = rep[lt.slot];
         if (a == b) continue;
         uint32_t na = 0, nb = 0;
         for (;;) {

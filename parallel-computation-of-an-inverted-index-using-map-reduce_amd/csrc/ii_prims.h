@@ -132,8 +132,16 @@ struct DigitOf {
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).
+// remap (optional, first pass of the token sort): the key's high word is an
+// index into remap, replaced by remap[high word] on load — fuses the
+// slot -> lexicographic-id step into the sort.
+__device__ __forceinline__ uint64_t remap_key(uint64_t k, const uint32_t* __restrict__ remap) {
+    return remap ? (((uint64_t)remap[k >> 32] << 32) | (k & 0xFFFFFFFFull)) : k;
+}
+
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
-                                                       int shift, uint32_t nchunks, uint64_t* __restrict__ table) {
+                                                       int shift, uint32_t nchunks, uint64_t* __restrict__ table,
+                                                       const uint32_t* __restrict__ remap) {
     __shared__ uint32_t cnt[kWaves][kRadix];
     for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&cnt[0][0])[i] = 0;
     __syncthreads();
@@ -142,11 +150,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
     // two keys per lane per step (16 B per lane)
     uint64_t i = lo + 2 * threadIdx.x;
     for (; i + 1 < hi; i += 2 * kBlock) {
-        uint64_t a = keys[i], b = keys[i + 1];
+        uint64_t a = remap_key(keys[i], remap), b = remap_key(keys[i + 1], remap);
         atomicAdd(&mine[(uint32_t)(a >> shift) & (kRadix - 1)], 1u);
         atomicAdd(&mine[(uint32_t)(b >> shift) & (kRadix - 1)], 1u);
     }
-    if (i < hi) atomicAdd(&mine[(uint32_t)(keys[i] >> shift) & (kRadix - 1)], 1u);
+    if (i < hi) atomicAdd(&mine[(uint32_t)(remap_key(keys[i], remap) >> shift) & (kRadix - 1)], 1u);
     __syncthreads();
     for (int d = threadIdx.x; d < kRadix; d += kBlock) {
         uint32_t t = 0;
@@ -164,7 +172,8 @@ template <bool kHasVals>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                           const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
                                                           uint64_t n, uint64_t chunk, int shift, uint32_t nchunks,
-                                                          const uint64_t* __restrict__ table) {
+                                                          const uint64_t* __restrict__ table,
+                                                          const uint32_t* __restrict__ remap) {
     __shared__ uint64_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[kHasVals ? kSortTile : 1];
     __shared__ uint32_t s_wcnt[kWaves][kRadix];
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
         for (int k = 0; k < kSortItems; k++) {
             uint64_t idx = wbase + (uint64_t)k * 64;
             bool valid = idx < hi;
-            key[k] = valid ? kin[idx] : ~0ull;
+            key[k] = valid ? remap_key(kin[idx], remap) : ~0ull;
             if (kHasVals) val[k] = valid ? vin[idx] : 0u;
         }
 #pragma unroll
