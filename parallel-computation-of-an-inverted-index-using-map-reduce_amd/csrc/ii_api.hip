@@ -44,7 +44,7 @@ struct ii_ctx {
     // K1
     DBuf rec, rec2, longs;
     DBuf tkeys, trep;
-    uint64_t table_cap = 1ull << 22;
+    uint64_t big_cap = 1ull << 22;  // big word table; total slots = kHotSlots + big_cap
     uint64_t long_cap = 0;
     uint64_t seed = 0x51ed270b27a3f3c1ull;
     // dictionary
@@ -221,7 +221,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
         return II_ERR_NOMEM;
     }
     const char* s = getenv("II_TABLE_LOG2");
-    if (s && atoi(s) >= 10 && atoi(s) <= 34) c->table_cap = 1ull << atoi(s);
+    if (s && atoi(s) >= 10 && atoi(s) <= 30) c->big_cap = 1ull << atoi(s);
     memset(&c->stats, 0, sizeof(c->stats));
     *out = c;
     return II_OK;
@@ -305,22 +305,23 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
 
     for (int attempt = 0;; attempt++) {
         if (attempt > 12) return II_ERR_INTERNAL;
-        if (c->table_cap > (1ull << 31)) return II_ERR_NOMEM;  // slots must fit 31 bits
-        CK(grow(c->tkeys, sizeof(uint64_t) * c->table_cap));
-        CK(grow(c->trep, sizeof(uint64_t) * c->table_cap));
+        if (c->big_cap > (1ull << 30)) return II_ERR_NOMEM;  // slots must fit 31 bits
+        const uint64_t nslots = kHotSlots + c->big_cap;
+        CK(grow(c->tkeys, sizeof(uint64_t) * nslots));
+        CK(grow(c->trep, sizeof(uint64_t) * nslots));
         CK(grow(c->longs, sizeof(LongTok) * c->long_cap));
-        HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * c->table_cap, c->st));
+        HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * nslots, c->st));
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
-        Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->table_cap - 1, c->seed, counters};
-        k_tok_emit<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
+        Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
+        k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<LongTok>(c->longs), c->long_cap);
         HIPCK(hipGetLastError());
-        CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, c->table_cap, counters + C_INSERT));
+        CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
         uint64_t cnt[4];
         CK(read_u64(c, counters, cnt, 4));
-        if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] * 2 > c->table_cap) {
-            c->table_cap *= 4;
+        if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] > kHotSlots / 2 + c->big_cap / 2) {
+            c->big_cap *= 4;
             c->retries++;
             continue;
         }
@@ -477,7 +478,8 @@ static int build_dictionary(ii_ctx* c) {
     CK(grow(c->dkey2, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->didx, sizeof(uint32_t) * (V + 1)));
     CK(grow(c->didx2, sizeof(uint32_t) * (V + 1)));
-    CK(grow(c->remap, sizeof(uint32_t) * c->table_cap));
+    const uint64_t nslots = kHotSlots + c->big_cap;
+    CK(grow(c->remap, sizeof(uint32_t) * nslots));
     CK(grow(c->lkey, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->lrep, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->llen, sizeof(uint32_t) * (V + 1)));
@@ -487,7 +489,7 @@ static int build_dictionary(ii_ctx* c) {
     const unsigned long long* keys = P_<unsigned long long>(c->tkeys);
     const uint64_t* rep = P_<uint64_t>(c->trep);
     uint32_t* dslot = P_<uint32_t>(c->dslot);
-    CK(run_scan(c, OpCompactSlots{keys, dslot}, c->table_cap, totals + 1));
+    CK(run_scan(c, OpCompactSlots{keys, dslot}, nslots, totals + 1));
     uint64_t vchk;
     CK(read_u64(c, totals + 1, &vchk));
     if (vchk != V) return II_ERR_INTERNAL;
@@ -853,7 +855,7 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
     s.tokens = c->T;
     s.words = c->V;
     s.long_tokens = c->nlong;
-    s.table_cap = c->table_cap;
+    s.table_cap = kHotSlots + c->big_cap;
     s.retries = c->retries;
     memcpy(s.letter_tokens, c->hist, sizeof(c->hist));
     s.ms_map = ev_ms(c->ev[0], c->ev[1]);

@@ -50,33 +50,82 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 // ---------------------------------------------------------------- word table
-// Open addressing, linear probing, 64-bit keys, 0 = empty.  Keys are exact for
-// words of <= 12 letters (5-bit letter codes, left aligned, low 4 bits 0) and a
-// 60-bit hash tagged 0xF for longer words (verified after the map, see
-// k_long_verify).  Keys never change once set, so a stale empty read is fixed
-// by the CAS.  The slot index is the word's provisional id.
+// Word identity -> slot (the word's provisional id).  Keys are exact for
+// words of <= 12 letters (5-bit letter codes, left aligned, low 4 bits 0) and
+// a 60-bit hash tagged 0xF for longer words (verified after the map, see
+// k_long_verify); 0 = empty.  Keys never change once set, so a stale empty
+// read is corrected by the CAS.
+//
+// Two levels, one slot space:
+//   hot table  slots [0, 2^17): 8-slot buckets (one 64-B line), probed inside
+//              the bucket only.  Words that arrive first — in a Zipf corpus
+//              mostly the frequent ones — fill it; 1 MB of keys stays in every
+//              XCD's 4 MB L2, so most probes never leave L2.
+//   big table  slots [2^17, 2^17 + cap): linear probing; words whose hot
+//              bucket was already full.
+// A word lives in exactly one place: a probe scans the same bucket (then the
+// same big-table run) in the same order and slots only go empty -> full.
+constexpr int kHotLog2 = 17;
+constexpr uint64_t kHotSlots = 1ull << kHotLog2;
+constexpr int kBucket = 8;
+
 struct Table {
-    unsigned long long* keys;
-    uint64_t* rep;      // token start of the inserting occurrence
-    uint64_t mask;
+    unsigned long long* keys;  // [kHotSlots + big_cap]
+    uint64_t* rep;             // token start of the inserting occurrence
+    uint64_t big_mask;         // big_cap - 1
     uint64_t seed;
     uint64_t* counters;
 };
 
-__device__ __forceinline__ uint32_t table_insert(const Table& t, uint64_t key, uint64_t pos) {
-    uint64_t h = mix64(key ^ t.seed) & t.mask;
+__device__ __forceinline__ uint64_t table_hash(const Table& t, uint64_t key) { return mix64(key ^ t.seed); }
+__device__ __forceinline__ uint64_t hot_home(uint64_t hh) { return hh & (kHotSlots - 1); }
+
+// CAS-insert key at empty slot s; returns the key now stored there.
+__device__ __forceinline__ unsigned long long table_claim(const Table& t, uint64_t s, uint64_t key, uint64_t pos) {
+    const unsigned long long old = atomicCAS(&t.keys[s], 0ull, (unsigned long long)key);
+    if (old == 0ull) {  // inserted; distinct words are counted later by a scan of the table
+        t.rep[s] = pos;
+        return key;
+    }
+    return old;
+}
+
+// Slot of key, inserting it if new.  Slow path of the probe (the home slot
+// did not hold the key): the 8-slot hot bucket (one 64-B line) and the word's
+// big-table home slot are loaded together, so a word living at its big-table
+// home costs one round trip; the bucket is scanned with bit masks in probe
+// order (home, home+1, ... within the bucket); a full bucket sends the word
+// to the big table (linear probing).
+__device__ __forceinline__ uint32_t table_find(const Table& t, uint64_t key, uint64_t hh, uint64_t pos) {
+    const uint64_t home = hot_home(hh);
+    const uint32_t h7 = (uint32_t)(home & (kBucket - 1));
+    const uint64_t bbase = home - h7;
+    uint64_t h = (hh >> 20) & t.big_mask;
+    const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(t.keys + bbase);
+    const ulonglong2 p0 = bp[0], p1 = bp[1], p2 = bp[2], p3 = bp[3];
+    unsigned long long kb = t.keys[kHotSlots + h];
+    const unsigned long long k[8] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
+    uint32_t match = 0, full = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        match |= (uint32_t)(k[j] == key) << j;
+        full |= (uint32_t)(k[j] != 0ull) << j;
+    }
+    if (match) return (uint32_t)(bbase + __builtin_ctz(match));
+    for (int it = 0; it < kBucket; it++) {
+        const uint32_t empty = ~full & 0xFFu;
+        if (!empty) break;
+        const uint32_t rot = ((empty >> h7) | (empty << (8 - h7))) & 0xFFu;
+        const uint32_t p = (h7 + __builtin_ctz(rot)) & (kBucket - 1);
+        if (table_claim(t, bbase + p, key, pos) == key) return (uint32_t)(bbase + p);
+        full |= 1u << p;
+    }
     for (int probe = 0; probe < kMaxProbe; probe++) {
-        unsigned long long k = t.keys[h];
-        if (k == key) return (uint32_t)h;
-        if (k == 0ull) {
-            unsigned long long old = atomicCAS(&t.keys[h], 0ull, (unsigned long long)key);
-            if (old == 0ull) {  // inserted; distinct words are counted later by a scan of the table
-                t.rep[h] = pos;
-                return (uint32_t)h;
-            }
-            if (old == key) return (uint32_t)h;
-        }
-        h = (h + 1) & t.mask;
+        const uint64_t s = kHotSlots + h;
+        if (probe) kb = t.keys[s];
+        if (kb == 0ull) kb = table_claim(t, s, key, pos);
+        if (kb == key) return (uint32_t)s;
+        h = (h + 1) & t.big_mask;
     }
     atomicOr((unsigned long long*)&t.counters[C_OVERFLOW], 1ull);
     return 0;
@@ -192,20 +241,33 @@ __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, uint64
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Stage text [tile_lo - 16, tile_lo + kTile + kHalo) into LDS with 16-B
-// loads; lane t's own window [tile_lo + 16t, +16) is returned in registers.
-// Bytes outside the text read as ' ' (so position 0 starts a token).
-__device__ __forceinline__ uint4 stage_tile(uint8_t* s_text, const uint8_t* __restrict__ text, uint64_t nbytes,
-                                            uint64_t tile_lo) {
+// Tile staging, software-pipelined: fetch_tile() loads the text of
+// [tile_lo - 16, tile_lo + kTile + kHalo) into registers (16 B per lane; lane
+// t's own window [tile_lo + 16t, +16) in .v, the left piece and the halo in
+// .h of lanes 0..32) one tile ahead; store_tile() writes them to LDS.  Bytes
+// outside the text read as ' ' (so position 0 starts a token).
+struct TileRegs {
+    uint4 v, h;
+};
+constexpr int kExtraPieces = 1 + kHalo / 16;  // left piece + halo pieces
+__device__ __forceinline__ TileRegs fetch_tile(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t tile_lo) {
     const int t = threadIdx.x;
-    const uint4 v = load16(text, nbytes, (int64_t)tile_lo + 16 * t);
-    *reinterpret_cast<uint4*>(s_text + 16 + 16 * t) = v;
-    constexpr int kExtra = 1 + kHalo / 16;  // left piece + halo pieces
-    if (t < kExtra) {
+    TileRegs r;
+    r.v = load16(text, nbytes, (int64_t)tile_lo + 16 * t);
+    r.h = make_uint4(0, 0, 0, 0);
+    if (t < kExtraPieces) {
         const int q = t == 0 ? -1 : kTile / 16 + t - 1;
-        *reinterpret_cast<uint4*>(s_text + 16 + 16 * q) = load16(text, nbytes, (int64_t)tile_lo + 16 * q);
+        r.h = load16(text, nbytes, (int64_t)tile_lo + 16 * q);
     }
-    return v;
+    return r;
+}
+__device__ __forceinline__ void store_tile(uint8_t* s_text, const TileRegs& r) {
+    const int t = threadIdx.x;
+    *reinterpret_cast<uint4*>(s_text + 16 + 16 * t) = r.v;
+    if (t < kExtraPieces) {
+        const int q = t == 0 ? -1 : kTile / 16 + t - 1;
+        *reinterpret_cast<uint4*>(s_text + 16 + 16 * q) = r.h;
+    }
 }
 
 __device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {
@@ -282,6 +344,94 @@ __device__ __forceinline__ uint32_t kept_starts(uint32_t starts, const Classes& 
     return kept | (starts & cl.letter);
 }
 
+// First 16 bytes of the token starting at window offset i (0..15), taken
+// from the lane's 32-byte view w[0..7] = own window + next lane's window.
+__device__ __forceinline__ uint32_t sel4(uint32_t k, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t lo = (k & 1u) ? b : a;  // two-level select: v_cndmask, no branches
+    const uint32_t hi = (k & 1u) ? d : c;
+    return (k & 2u) ? hi : lo;
+}
+__device__ __forceinline__ uint4 token_bytes(const uint32_t (&w)[8], uint32_t i) {
+    const uint32_t wo = i >> 2, bo = i & 3;
+    uint32_t x[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) x[j] = sel4(wo, w[j], w[j + 1], w[j + 2], w[j + 3]);
+    return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], bo), __builtin_amdgcn_alignbyte(x[2], x[1], bo),
+                      __builtin_amdgcn_alignbyte(x[3], x[2], bo), __builtin_amdgcn_alignbyte(x[4], x[3], bo));
+}
+
+// Register fast path of the cleaning loop (main.c:105-111) for the common
+// token: it ends (whitespace / NUL) inside its first 16 bytes and its letters
+// form one run from its first byte (plain or capitalised words, trailing
+// punctuation) with at most 12 letters.  Returns false otherwise.
+__device__ __forceinline__ bool fast_key(const uint4& tb, TokKey& out) {
+    const Classes c = classify16(tb);
+    const uint32_t term = c.ws | c.nul;
+    if (term == 0) return false;
+    const uint32_t e = __builtin_ctz(term);
+    const uint32_t lm = c.letter & ((1u << e) - 1u);
+    const uint32_t n = __popc(lm);
+    if (n == 0 || n > 12 || lm != (1u << n) - 1u) return false;
+    const uint32_t w[3] = {(tb.x | 0x20202020u) & 0x1F1F1F1Fu, (tb.y | 0x20202020u) & 0x1F1F1F1Fu,
+                           (tb.z | 0x20202020u) & 0x1F1F1F1Fu};
+    uint64_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) packed |= (uint64_t)((w[k >> 2] >> (8 * (k & 3))) & 31u) << (59 - 5 * k);
+    out.key = packed & (~0ull << (64 - 5 * n));
+    out.nlet = n;
+    out.first = (w[0] & 31u) - 1u;
+    return true;
+}
+
+// 16 bytes of the staged tile at tile-local position p (any alignment):
+// two aligned LDS reads + byte shift; past the staged halo, global memory.
+__device__ __forceinline__ uint4 tile_block16(const uint8_t* s_text, const uint8_t* __restrict__ text, uint64_t nbytes,
+                                              uint64_t tile_lo, uint32_t p) {
+    const uint32_t a = 16 + p;
+    const uint32_t base = a & ~15u;
+    if (base + 32 <= (uint32_t)(16 + kTile + kHalo)) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(s_text + base);
+        const uint4 hi = *reinterpret_cast<const uint4*>(s_text + base + 16);
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        return token_bytes(w, a & 15u);
+    }
+    return load16(text, nbytes, (int64_t)tile_lo + p);
+}
+
+__device__ __forceinline__ uint32_t byte_dyn(const uint4& b, uint32_t j) {
+    return (sel4(j >> 2, b.x, b.y, b.z, b.w) >> (8 * (j & 3u))) & 0xFFu;
+}
+
+// General form of the cleaning loop (main.c:105-111): 16 bytes per step,
+// SWAR classes, then only the letter bytes are visited.  Stops at whitespace,
+// NUL or the 299th letter.  first16 = the token's first 16 bytes.
+__device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, const uint8_t* __restrict__ text,
+                                              uint64_t nbytes, uint64_t tile_lo, uint32_t p, uint64_t seed) {
+    uint64_t packed = 0, hash = 1469598103934665603ull;
+    uint32_t n = 0, first = 0;
+    for (;;) {
+        const Classes cl = classify16(b);
+        const uint32_t term = cl.ws | cl.nul;
+        const uint32_t e = term ? __builtin_ctz(term) : 16u;
+        bool done = term != 0;
+        for (uint32_t m = cl.letter & ((1u << e) - 1u); m; m &= m - 1) {
+            const uint32_t lc = (byte_dyn(b, __builtin_ctz(m)) | 0x20u) - 0x61u;
+            if (n == 0) first = lc;
+            n++;
+            if (n <= 12) packed |= (uint64_t)(lc + 1) << (64 - 5 * n);
+            hash = (hash ^ (lc + 1)) * 1099511628211ull;
+            if (n == (uint32_t)kMaxWord) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        p += 16;
+        b = tile_block16(s_text, text, nbytes, tile_lo, p);
+    }
+    return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
+}
+
 // K1a: kept tokens per 64 KiB chunk -> chunk_cnt[blockIdx.x].
 __global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                       uint64_t* __restrict__ chunk_cnt) {
@@ -291,9 +441,12 @@ __global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict_
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
     const uint32_t wlo = (uint32_t)threadIdx.x * 16;
     uint64_t kept = 0;
+    TileRegs nxt = fetch_tile(text, nbytes, chunk_lo);
     for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
         __syncthreads();
-        const uint4 v = stage_tile(s_text, text, nbytes, tile_lo);
+        store_tile(s_text, nxt);
+        const uint4 v = nxt.v;
+        if (tile_lo + kTile < chunk_hi) nxt = fetch_tile(text, nbytes, tile_lo + kTile);
         __syncthreads();
         const Classes cl = classify16(v);
         kept += __popc(kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo));
@@ -310,24 +463,18 @@ struct LongTok {
 };
 constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 
-// Probe / insert starting from home slot h with the key at slot h already read.
-__device__ __forceinline__ uint32_t table_resolve(const Table& t, uint64_t key, uint64_t h, unsigned long long k,
-                                                  uint64_t pos) {
-    for (int probe = 0; probe < kMaxProbe; probe++) {
-        if (k == key) return (uint32_t)h;
-        if (k == 0ull) {
-            unsigned long long old = atomicCAS(&t.keys[h], 0ull, (unsigned long long)key);
-            if (old == 0ull) {
-                t.rep[h] = pos;
-                return (uint32_t)h;
-            }
-            if (old == key) return (uint32_t)h;
-        }
-        h = (h + 1) & t.mask;
-        k = t.keys[h];
+// Queue a long token for k_long_verify: into the workgroup's LDS buffer, or
+// straight to global memory when the tile alone overflows the buffer.
+__device__ __forceinline__ void queue_long(bool direct, LongTok* s_long, uint32_t* s_lcount, uint64_t lbase,
+                                           LongTok* __restrict__ longs, uint64_t long_cap, const Table& tab, uint64_t pos,
+                                           uint32_t slot) {
+    if (direct) {
+        const uint64_t li = lbase + atomicAdd(s_lcount, 1u);
+        if (li < long_cap) longs[li] = LongTok{pos, slot};
+        else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+    } else {
+        s_long[atomicAdd(s_lcount, 1u)] = LongTok{pos, slot};
     }
-    atomicOr((unsigned long long*)&t.counters[C_OVERFLOW], 1ull);
-    return 0;
 }
 
 // K1b: chunk_off holds exclusive record offsets.  Per 4 KiB tile:
@@ -339,6 +486,10 @@ __device__ __forceinline__ uint32_t table_resolve(const Table& t, uint64_t key, 
 // First letters are counted per chunk (chunk_hist[chunk][26] = the
 // partial_<letter>.txt line counts); tokens of > 12 letters are queued for the
 // hash-collision check.  No global atomics on a shared word per token.
+// kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
+// bit 0 = skip the table probe, bit 1 = skip the token walk, bit 2 = skip the
+// letter histogram, bit 3 = no long-token queue, bit 4 = fast path only.
+template <int kAblate = 0>
 __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                      const uint64_t* __restrict__ file_start,
                                                      const uint32_t* __restrict__ file_id, uint32_t nfiles,
@@ -349,6 +500,8 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
     __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
     __shared__ uint64_t s_key[kMaxTok];   // word key, then the record
     __shared__ uint16_t s_off[kMaxTok];   // tile offset | 0x8000 if long
+    __shared__ uint16_t s_slow[kMaxTok];  // tokens for the general key path
+    __shared__ uint32_t s_nslow, s_nmiss;
     __shared__ LongTok s_long[kLongBuf];
     __shared__ uint64_t s_scan[kWaves + 1];
     __shared__ uint32_t s_hist[32];
@@ -368,27 +521,58 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
     uint64_t out = chunk_off[blockIdx.x];
     const uint32_t wlo = (uint32_t)t * 16;
 
+    TileRegs nxt = fetch_tile(text, nbytes, chunk_lo);
     for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
         __syncthreads();
-        const uint4 v = stage_tile(s_text, text, nbytes, tile_lo);
+        store_tile(s_text, nxt);
+        const uint4 v = nxt.v;
+        if (tile_lo + kTile < chunk_hi) nxt = fetch_tile(text, nbytes, tile_lo + kTile);
         __syncthreads();
         // 1. kept starts
+        if (t == 0) s_nslow = s_nmiss = 0;
         const Classes cl = classify16(v);
         const uint32_t kept = kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo);
         uint64_t tot;
         uint32_t o = (uint32_t)block_excl_scan(__popc(kept), &tot, s_scan);
-        // 2. walk
+        // 2a. word keys, register fast path; the rest go to a compact list
         uint32_t nlong = 0;
         {
-            TileReader rd(s_text, text, nbytes, tile_lo);
+            const uint4 nx = *reinterpret_cast<const uint4*>(s_text + 16 + wlo + 16);  // next lane's window
+            const uint32_t w8[8] = {v.x, v.y, v.z, v.w, nx.x, nx.y, nx.z, nx.w};
             for (uint32_t m = kept; m; m &= m - 1) {
                 const uint32_t i = __builtin_ctz(m);
-                const TokKey k = token_key(rd, wlo + i, tab.seed);
-                atomicAdd(&s_hist[k.first], 1u);
-                s_key[o] = k.key;
-                s_off[o] = (uint16_t)((wlo + i) | (k.nlet > 12 ? 0x8000u : 0u));
-                nlong += k.nlet > 12;
+                TokKey k;
+                bool ok;
+                if (kAblate & 2) {
+                    k = TokKey{(uint64_t)(wlo + i + 1) << 8, 3u, i % 26u};
+                    ok = true;
+                } else {
+                    ok = fast_key(token_bytes(w8, i), k);
+                }
+                s_off[o] = (uint16_t)(wlo + i);
+                if (ok) {
+                    if (!(kAblate & 4)) atomicAdd(&s_hist[k.first], 1u);
+                    s_key[o] = k.key;
+                } else {
+                    s_slow[atomicAdd(&s_nslow, 1u)] = (uint16_t)o;
+                }
                 o++;
+            }
+        }
+        __syncthreads();
+        // 2b. general path (inner punctuation, > 12 letters, > 16 bytes), one token per thread
+        for (uint32_t q = t; q < s_nslow; q += kBlock) {
+            const uint32_t j = s_slow[q];
+            const uint32_t p = s_off[j];
+            TokKey k = (kAblate & 16) ? TokKey{(uint64_t)(p + 1) << 8, 3u, p % 26u}
+                                      : general_key(tile_block16(s_text, text, nbytes, tile_lo, p), s_text, text, nbytes,
+                                                    tile_lo, p, tab.seed);
+            if (kAblate & 8) k.nlet = k.nlet > 12 ? 12 : k.nlet;
+            if (!(kAblate & 4)) atomicAdd(&s_hist[k.first], 1u);
+            s_key[j] = k.key;
+            if (k.nlet > 12) {
+                s_off[j] = (uint16_t)(p | 0x8000u);
+                nlong++;
             }
         }
         uint64_t ltot;
@@ -409,8 +593,10 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
             }
             __syncthreads();
         }
-        // 3. probe: token q = t + u*kBlock, four loads in flight per thread
+        // 3a. probe the hot-table home slot: token q = t + u*kBlock, four
+        //     loads in flight per thread; misses go to a compact list
         const uint32_t ntok = (uint32_t)tot;
+        const uint32_t fsame = s_f[0] == s_f[1];
         for (uint32_t base = t; base < ntok; base += 4 * kBlock) {
             uint64_t key[4], h[4];
             unsigned long long kk[4];
@@ -418,29 +604,38 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
             for (int u = 0; u < 4; u++) {
                 const uint32_t q = base + u * kBlock;
                 key[u] = q < ntok ? s_key[q] : 0ull;
-                h[u] = mix64(key[u] ^ tab.seed) & tab.mask;
+                h[u] = table_hash(tab, key[u]);
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) kk[u] = (base + u * kBlock < ntok) ? tab.keys[h[u]] : 0ull;
+            for (int u = 0; u < 4; u++)
+                kk[u] = (kAblate & 1) ? key[u] : (base + u * kBlock < ntok) ? tab.keys[hot_home(h[u])] : 0ull;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t q = base + u * kBlock;
                 if (q >= ntok) continue;
+                if (kk[u] != key[u]) {
+                    s_slow[atomicAdd(&s_nmiss, 1u)] = (uint16_t)q;
+                    continue;
+                }
                 const uint32_t off = s_off[q];
                 const uint64_t pos = tile_lo + (off & 0x7FFFu);
-                const uint32_t slot = kk[u] == key[u] ? (uint32_t)h[u] : table_resolve(tab, key[u], h[u], kk[u], pos);
-                const uint32_t f = s_f[0] == s_f[1] ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
+                const uint32_t slot = (uint32_t)hot_home(h[u]);
+                const uint32_t f = fsame ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
                 s_key[q] = ((uint64_t)slot << 32) | file_id[f];
-                if (off & 0x8000u) {
-                    if (direct) {
-                        const uint64_t li = s_lbase + atomicAdd(&s_lcount, 1u);
-                        if (li < long_cap) longs[li] = LongTok{pos, slot};
-                        else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-                    } else {
-                        s_long[atomicAdd(&s_lcount, 1u)] = LongTok{pos, slot};
-                    }
-                }
+                if (off & 0x8000u) queue_long(direct, s_long, &s_lcount, s_lbase, longs, long_cap, tab, pos, slot);
             }
+        }
+        __syncthreads();
+        // 3b. misses, one per thread: bucket line + big-table home in one round trip
+        for (uint32_t r = t; r < s_nmiss; r += kBlock) {
+            const uint32_t q = s_slow[r];
+            const uint64_t key = s_key[q];
+            const uint32_t off = s_off[q];
+            const uint64_t pos = tile_lo + (off & 0x7FFFu);
+            const uint32_t slot = table_find(tab, key, table_hash(tab, key), pos);
+            const uint32_t f = fsame ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
+            s_key[q] = ((uint64_t)slot << 32) | file_id[f];
+            if (off & 0x8000u) queue_long(direct, s_long, &s_lcount, s_lbase, longs, long_cap, tab, pos, slot);
         }
         __syncthreads();
         if (direct && t == 0) s_lcount = 0;

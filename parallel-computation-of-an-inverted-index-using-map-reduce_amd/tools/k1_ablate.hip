@@ -1,0 +1,72 @@
+// k1_ablate.hip — timing experiment for the K1 emit kernel (not product code).
+// Times k_tok_emit<kAblate> variants on one synthetic Zipf corpus:
+//   0 full, 1 no table probe, 2 no token walk, 3 neither; and k_tok_count.
+// Usage: k1_ablate [bytes] [files] [vocab]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+#include "../csrc/ii_kernels.h"
+using namespace ii;
+
+typedef struct { uint64_t total_bytes; uint32_t nfiles, vocab; uint64_t seed; double size_sigma; } iigen_params;
+extern "C" int iigen_layout(const iigen_params*, uint64_t*);
+extern "C" int iigen_fill(const iigen_params*, const uint64_t*, uint8_t*, int);
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+template <int A>
+float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, uint32_t nf, uint64_t* chunk_off,
+          Table tab, uint64_t nslots, uint64_t* rec, uint32_t* chist, LongTok* longs, uint64_t lcap, uint64_t nch) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    float best = 1e9;
+    for (int it = 0; it < 4; it++) {
+        CK(hipMemset(tab.keys, 0, nslots * 8));
+        CK(hipMemset(tab.counters, 0, 8 * C_NUM));
+        CK(hipEventRecord(a));
+        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, tab, rec, chist, longs, lcap);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
+    }
+    return best;
+}
+
+int main(int argc, char** argv) {
+    iigen_params p = {argc > 1 ? strtoull(argv[1], 0, 10) : 1000000000ull, argc > 2 ? (uint32_t)atoi(argv[2]) : 1000u,
+                      argc > 3 ? (uint32_t)atoi(argv[3]) : 1000000u, 3, 1.0};
+    std::vector<uint64_t> off(p.nfiles + 1);
+    std::vector<uint8_t> text(p.total_bytes + 16);
+    iigen_layout(&p, off.data());
+    iigen_fill(&p, off.data(), text.data(), 16);
+    const uint64_t nb = p.total_bytes, nch = (nb + kChunk - 1) / kChunk;
+    uint8_t* d_text; uint64_t *fstart, *chunk, *rec, *counters; uint32_t *fid, *chist; LongTok* longs;
+    unsigned long long* keys; uint64_t* rep;
+    const uint64_t big = 1ull << 22, nslots = kHotSlots + big, lcap = 1ull << 24;
+    CK(hipMalloc(&d_text, nb + 64)); CK(hipMemcpy(d_text, text.data(), nb, hipMemcpyHostToDevice));
+    std::vector<uint32_t> ids(p.nfiles);
+    for (uint32_t i = 0; i < p.nfiles; i++) ids[i] = i;
+    CK(hipMalloc(&fstart, 8 * p.nfiles)); CK(hipMemcpy(fstart, off.data(), 8 * p.nfiles, hipMemcpyHostToDevice));
+    CK(hipMalloc(&fid, 4 * p.nfiles)); CK(hipMemcpy(fid, ids.data(), 4 * p.nfiles, hipMemcpyHostToDevice));
+    CK(hipMalloc(&chunk, 8 * nch)); CK(hipMalloc(&chist, 4 * 26 * nch)); CK(hipMalloc(&counters, 8 * C_NUM));
+    CK(hipMalloc(&keys, 8 * nslots)); CK(hipMalloc(&rep, 8 * nslots)); CK(hipMalloc(&longs, sizeof(LongTok) * lcap));
+    // count pass -> offsets (host scan)
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    k_tok_count<<<(uint32_t)nch, kBlock>>>(d_text, nb, chunk);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms_count; CK(hipEventElapsedTime(&ms_count, a, b));
+    std::vector<uint64_t> cnt(nch);
+    CK(hipMemcpy(cnt.data(), chunk, 8 * nch, hipMemcpyDeviceToHost));
+    uint64_t T = 0;
+    for (auto& c : cnt) { uint64_t x = c; c = T; T += x; }
+    CK(hipMemcpy(chunk, cnt.data(), 8 * nch, hipMemcpyHostToDevice));
+    CK(hipMalloc(&rec, 8 * T));
+    Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters};
+#define RUN(A) printf("emit ablate %2d: %.3f ms\n", A, run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch))
+    printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
+    RUN(0); RUN(1); RUN(2); RUN(3); RUN(5); RUN(9); RUN(17); RUN(29); RUN(28); RUN(12); RUN(16);
+    return 0;
+}

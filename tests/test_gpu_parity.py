@@ -136,17 +136,20 @@ def test_noncontiguous_ids(idx):
 
 
 def test_table_regrow_and_reuse():
-    os.environ["II_TABLE_LOG2"] = "10"  # 1024 slots: forces several regrows
+    os.environ["II_TABLE_LOG2"] = "10"  # 1024-slot big table: forces several regrows
     try:
         ix = ii_ctypes.Index(0)
     finally:
         del os.environ["II_TABLE_LOG2"]
-    text, off, ids, expected = case_arrays("zipf_small")
+    t, off = ii_ctypes.zipf_corpus(24_000_000, 300, 400_000, 5, threads=8)
+    ids = list(range(300))
+    exp = oracle_index(t, off, ids)
     for _ in range(2):
-        ix.map_host(text, off, ids)
+        ix.map_host(t, off.tolist(), ids)
         ix.reduce()
-        assert_same(ix.letters(), expected, "regrow")
-    assert ix.stats().table_cap >= 2 * ix.stats().words
+        assert_same(ix.letters(), exp, "regrow")
+    st = ix.stats()
+    assert st.words > 131072 and st.table_cap >= 2 * st.words
     ix.close()
 
 
