@@ -48,6 +48,22 @@ def parse():
     return p.parse_args()
 
 
+def pmc_traffic():
+    """HBM bytes per launch by kernel from the committed rocprofv3 PMC summary
+    of this same bench command (profiles/*_pmc_traffic.json, newest round),
+    corrected as profiles/pmc_traffic.py documents; {} when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return {}
+    try:
+        d = json.load(open(files[-1]))
+        return {k: round(v["traffic_bytes_per_launch"]) for k, v in d["kernels"].items()
+                if "traffic_bytes_per_launch" in v}
+    except Exception:
+        return {}
+
+
 def safe_mappers(sizes, cores):
     """Largest M <= cores for which the reference's greedy split (main.c:307-323)
     initialises every mapper's range; with more mappers than realised shards
@@ -153,11 +169,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scatter_ms = []
+    scatter_ms, emit_ms = [], []
     for _ in range(a.steps):
         step()
         st = idx.stats()
         scatter_ms.append(st.scatter_ms_avg)
+        emit_ms.append(st.emit_ms)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,7 +190,10 @@ def main():
 
     if rank == 0:
         sc_ms = sum(scatter_ms) / len(scatter_ms)
-        achieved = st.scatter_bytes / (sc_ms * 1e-3) / 1e9 if sc_ms > 0 else 0.0
+        sc_achieved = st.scatter_bytes / (sc_ms * 1e-3) / 1e9 if sc_ms > 0 else 0.0
+        em_ms = sum(emit_ms) / len(emit_ms)
+        em_achieved = st.emit_bytes / (em_ms * 1e-3) / 1e9 if em_ms > 0 else 0.0
+        traffic = pmc_traffic()
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(text, off, a.cpu_sample_bytes)
         line = {
             "metric": "indexed input GB/s (whole node) + % of HBM peak BW",
@@ -191,10 +211,16 @@ def main():
             "config": {"workload": "zipf %.0f GB x %d files/rank, vocab %d (BASELINE configs[2])" % (
                 nbytes / 1e9, a.files, a.vocab), "bytes_per_rank": nbytes, "files_per_rank": a.files,
                 "vocab": a.vocab, "parallelism": "shard-per-gpu x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_radix_scatter (token sort pass)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
+            # dominant kernel: the tokenizer (K1b); algorithmic bytes = B + 8*T per launch
+            "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
+                         "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(em_achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic.get("ii::k_tok_emit<0>"),
+                         "bytes_per_launch": st.emit_bytes, "ms_per_launch": round(em_ms, 4)},
+            "roofline_sort": {"bound": "hbm", "kernel": "k_radix_scatter (token sort passes)",
+                              "achieved": round(sc_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(sc_achieved / HBM_PEAK_GBS, 4),
+                              "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
             "cpu_baseline": cpu,
             "phases_ms": {k: round(getattr(st, k), 3) for k in
                           ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total"]},

@@ -74,8 +74,12 @@ typedef struct {
     double ms_total;
     /* dominant kernel: the radix scatter of the token sort */
     double scatter_ms_avg; /* average duration of one token-sort scatter launch */
-    uint64_t scatter_bytes;/* algorithmic bytes of one token-sort scatter launch */
+    uint64_t scatter_bytes;/* average algorithmic bytes of one token-sort scatter launch */
     uint32_t scatter_launches;
+    uint64_t sorted_records; /* records left after the sort's first-pass (hot word, file) dedup */
+    /* tokenizer kernel (K1b k_tok_emit), the dominant kernel */
+    double emit_ms;        /* duration of the last k_tok_emit launch */
+    uint64_t emit_bytes;   /* its algorithmic bytes: B text read + 8 B per record written */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

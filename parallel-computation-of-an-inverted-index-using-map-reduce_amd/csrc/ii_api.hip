@@ -68,8 +68,11 @@ struct ii_ctx {
     bool host_valid = false;
 
     hipEvent_t ev[8] = {};
+    hipEvent_t ev_emit[2] = {};  // around the last (successful) k_tok_emit launch
     hipEvent_t ev_sc[2 * kMaxTimedPasses] = {};
+    uint64_t sc_bytes[kMaxTimedPasses] = {0};  // algorithmic bytes of each timed scatter launch
     int n_sc = 0;
+    uint64_t T_sorted = 0;  // records left after the pass-0 dedup
     ii_stats stats;
 };
 
@@ -117,6 +120,12 @@ static inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t
 static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 
 // ----------------------------------------------------------------- scan / sort
+static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
+    HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    HIPCK(hipStreamSynchronize(c->st));
+    return II_OK;
+}
+
 template <class Op>
 static int run_scan(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
     if (n == 0) {
@@ -159,28 +168,47 @@ struct OpInPlace {
 
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
+// With dedup0 (token sort only) the first pass also drops repeated
+// (hot word, file) records; *n_out receives the number of records kept.
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
-                    bool timed, int* passes, const uint32_t* remap0 = nullptr) {
+                    bool timed, int* passes, const uint32_t* remap0 = nullptr, bool dedup0 = false,
+                    uint64_t* n_out = nullptr) {
     if (passes) *passes = 0;
+    if (n_out) *n_out = n;
     if (n <= 1 || hi <= lo) return II_OK;
+    uint64_t n_kept = n;  // records surviving the pass-0 dedup
     uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
     uint64_t chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
     nch = (n + chunk - 1) / chunk;
     CK(grow(c->rtable, sizeof(uint64_t) * kRadix * nch));
     uint64_t* table = P_<uint64_t>(c->rtable);
     const bool kv = v != nullptr;
+    uint64_t* totals = P_<uint64_t>(c->totals);
     for (int shift = lo; shift < hi; shift += kRadixBits) {
         const uint32_t* remap = shift == lo ? remap0 : nullptr;
-        k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
-        CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
+        const bool dd = dedup0 && shift == lo;
+        if (shift != lo && n != n_kept) {  // records were dropped: regrid the remaining passes
+            n = n_kept;
+            if (n <= 1) break;
+            nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
+            chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
+            nch = (n + chunk - 1) / chunk;
+        }
+        if (dd) k_radix_hist<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
+        else k_radix_hist<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
+        CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, dd ? totals + 4 : nullptr));
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
         if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
+        const uint64_t n_in = n;
         if (kv)
-            k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift, (uint32_t)nch, table,
-                                                                       remap);
+            k_radix_scatter<true, false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift,
+                                                                              (uint32_t)nch, table, remap);
+        else if (dd)
+            k_radix_scatter<false, true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
+                                                                              (uint32_t)nch, table, remap);
         else
-            k_radix_scatter<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
-                                                                        (uint32_t)nch, table, remap);
+            k_radix_scatter<false, false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
+                                                                               (uint32_t)nch, table, remap);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
             c->n_sc++;
@@ -189,13 +217,10 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         std::swap(*k, *k2);
         if (kv) std::swap(*v, *v2);
         if (passes) (*passes)++;
+        if (dd) CK(read_u64(c, totals + 4, &n_kept));
+        if (ev) c->sc_bytes[c->n_sc - 1] = 8 * n_in + 8 * (dd ? n_kept : n_in) + (kv ? 8 * n_in : 0);
     }
-    return II_OK;
-}
-
-static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
-    HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
-    HIPCK(hipStreamSynchronize(c->st));
+    if (n_out) *n_out = n_kept;
     return II_OK;
 }
 
@@ -215,6 +240,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     HIPCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
+    for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
     if (grow(c->partial, sizeof(uint64_t) * (kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
@@ -243,6 +269,8 @@ extern "C" void ii_close(ii_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_sc)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_emit)
         if (e) (void)hipEventDestroy(e);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
@@ -275,7 +303,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
     uint64_t* totals = P_<uint64_t>(c->totals);
     HIPCK(hipEventRecord(c->ev[0], c->st));
     HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
-    c->T = c->V = c->U = c->nlong = 0;
+    c->T = c->V = c->U = c->nlong = c->T_sorted = 0;
     if (c->nbytes == 0 || c->nfiles == 0) {
         memset(c->hist, 0, sizeof(c->hist));
         if (hist_out) memset(hist_out, 0, sizeof(uint64_t) * II_ALPHABET);
@@ -313,9 +341,11 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * nslots, c->st));
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
+        HIPCK(hipEventRecord(c->ev_emit[0], c->st));
         k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<LongTok>(c->longs), c->long_cap);
+        HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
         uint64_t cnt[4];
@@ -578,16 +608,18 @@ static int local_reduce(ii_ctx* c) {
         k_remap<<<1, kBlock, 0, c->st>>>(r, T, P_<uint32_t>(c->remap));
         HIPCK(hipGetLastError());
     }
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap)));
+    uint64_t Tk = T;
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap), true, &Tk));
     c->rec_sorted = r;
+    c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
 
     // ---- K3: unique (word, file) pairs and posting starts
-    CK(grow(c->uniq, sizeof(uint64_t) * T));
+    CK(grow(c->uniq, sizeof(uint64_t) * Tk));
     CK(grow(c->pstart, sizeof(uint64_t) * (V + 1)));
     uint64_t* uniq = P_<uint64_t>(c->uniq);
     uint64_t* ps = P_<uint64_t>(c->pstart);
-    CK(run_scan(c, OpUnique{r, uniq, ps}, T, ps + V));
+    CK(run_scan(c, OpUnique{r, uniq, ps}, Tk, ps + V));
     CK(read_u64(c, ps + V, &c->U));
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;
@@ -859,6 +891,10 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
     s.retries = c->retries;
     memcpy(s.letter_tokens, c->hist, sizeof(c->hist));
     s.ms_map = ev_ms(c->ev[0], c->ev[1]);
+    if (c->T) {
+        s.emit_ms = ev_ms(c->ev_emit[0], c->ev_emit[1]);
+        s.emit_bytes = c->nbytes + 8 * c->T;  // tokenize = B + r*T, r = 8-byte record
+    }
     if (c->reduced) {
         s.pairs = c->U;
         s.out_bytes = c->out_bytes;
@@ -870,10 +906,15 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.ms_format = ev_ms(c->ev[5], c->ev[6]);
         s.ms_total = ev_ms(c->ev[0], c->ev[6]);
         double sum = 0;
-        for (int i = 0; i < c->n_sc; i++) sum += ev_ms(c->ev_sc[2 * i], c->ev_sc[2 * i + 1]);
+        uint64_t bytes = 0;
+        for (int i = 0; i < c->n_sc; i++) {
+            sum += ev_ms(c->ev_sc[2 * i], c->ev_sc[2 * i + 1]);
+            bytes += c->sc_bytes[i];
+        }
         s.scatter_launches = (uint32_t)c->n_sc;
         s.scatter_ms_avg = c->n_sc ? sum / c->n_sc : 0;
-        s.scatter_bytes = 16ull * c->T;  // read 8 B + write 8 B per record
+        s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: 8 B read per record in, 8 B written per record out
+        s.sorted_records = c->T_sorted;
     }
     *o = s;
     return II_OK;
