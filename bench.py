@@ -223,9 +223,11 @@ def main():
                               "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
             "cpu_baseline": cpu,
             "phases_ms": {k: round(getattr(st, k), 3) for k in
-                          ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total"]},
+                          ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total",
+                           "emit_ms", "resolve_ms"]},
             "counts": {"tokens": st.tokens, "pairs": st.pairs, "words": st.words, "long_tokens": st.long_tokens,
-                       "out_bytes": st.out_bytes, "sort_passes": st.sort_passes, "table_cap": st.table_cap},
+                       "out_bytes": st.out_bytes, "sort_passes": st.sort_passes, "table_cap": st.table_cap,
+                       "resolved_tokens": st.resolved_tokens, "sorted_records": st.sorted_records},
             "gen_seconds": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)

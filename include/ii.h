@@ -80,6 +80,8 @@ typedef struct {
     /* tokenizer kernel (K1b k_tok_emit), the dominant kernel */
     double emit_ms;        /* duration of the last k_tok_emit launch */
     uint64_t emit_bytes;   /* its algorithmic bytes: B text read + 8 B per record written */
+    double resolve_ms;     /* K1c k_tok_resolve (tokens the emit kernel left unresolved) */
+    uint64_t resolved_tokens; /* tokens K1b handed to K1c (general path, full hot bucket, raced claim) */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

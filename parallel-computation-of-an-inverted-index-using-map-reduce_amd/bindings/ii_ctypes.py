@@ -34,7 +34,8 @@ class Stats(ctypes.Structure):
         ("ms_reduce", ctypes.c_double), ("ms_order", ctypes.c_double), ("ms_format", ctypes.c_double),
         ("ms_total", ctypes.c_double), ("scatter_ms_avg", ctypes.c_double), ("scatter_bytes", ctypes.c_uint64),
         ("scatter_launches", ctypes.c_uint32), ("sorted_records", ctypes.c_uint64),
-        ("emit_ms", ctypes.c_double), ("emit_bytes", ctypes.c_uint64),
+        ("emit_ms", ctypes.c_double), ("emit_bytes", ctypes.c_uint64), ("resolve_ms", ctypes.c_double),
+        ("resolved_tokens", ctypes.c_uint64),
     ]
 
     def as_dict(self):

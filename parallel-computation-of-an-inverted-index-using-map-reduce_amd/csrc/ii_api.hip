@@ -42,7 +42,7 @@ struct ii_ctx {
     // scratch
     DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable;
     // K1
-    DBuf rec, rec2, longs;
+    DBuf rec, rec2, longs, pend, pend_cnt;
     DBuf tkeys, trep;
     uint64_t big_cap = 1ull << 22;  // big word table; total slots = kHotSlots + big_cap
     uint64_t long_cap = 0;
@@ -69,10 +69,12 @@ struct ii_ctx {
 
     hipEvent_t ev[8] = {};
     hipEvent_t ev_emit[2] = {};  // around the last (successful) k_tok_emit launch
+    hipEvent_t ev_res[2] = {};   // [1]: after the k_tok_resolve launch that follows k_tok_emit
     hipEvent_t ev_sc[2 * kMaxTimedPasses] = {};
     uint64_t sc_bytes[kMaxTimedPasses] = {0};  // algorithmic bytes of each timed scatter launch
     int n_sc = 0;
     uint64_t T_sorted = 0;  // records left after the pass-0 dedup
+    uint64_t n_pending = 0; // tokens K1b left to K1c
     ii_stats stats;
 };
 
@@ -160,6 +162,12 @@ static int run_reduce(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
     return II_OK;
 }
 
+struct OpU32 {
+    const uint32_t* a;
+    __device__ uint64_t value(uint64_t i) const { return a[i]; }
+    __device__ void emit(uint64_t, uint64_t, uint64_t) const {}
+};
+
 struct OpInPlace {
     uint64_t* a;
     __device__ uint64_t value(uint64_t i) const { return a[i]; }
@@ -241,6 +249,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
+    for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
     if (grow(c->partial, sizeof(uint64_t) * (kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
@@ -263,7 +272,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
-                   &c->woff,     &c->pts};
+                   &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -271,6 +280,8 @@ extern "C" void ii_close(ii_ctx* c) {
     for (auto& e : c->ev_sc)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_emit)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_res)
         if (e) (void)hipEventDestroy(e);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
@@ -329,6 +340,8 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
     c->T = hv[0];
     CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
     CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+    CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
+    CK(grow(c->pend_cnt, sizeof(uint32_t) * nch));
     if (c->long_cap < std::max<uint64_t>(1 << 16, c->T / 64)) c->long_cap = std::max<uint64_t>(1 << 16, c->T / 64);
 
     for (int attempt = 0;; attempt++) {
@@ -344,8 +357,14 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
         k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                       P_<LongTok>(c->longs), c->long_cap);
+                                                       P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt));
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
+        k_tok_resolve<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
+                                                           P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
+                                                           P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
+                                                           P_<LongTok>(c->longs), c->long_cap);
+        HIPCK(hipEventRecord(c->ev_res[1], c->st));
+        CK(run_reduce(c, OpU32{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
         uint64_t cnt[4];
@@ -374,6 +393,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
             }
         }
         c->V = cnt[C_INSERT];
+        CK(read_u64(c, totals + 5, &c->n_pending));
         break;
     }
     k_hist_reduce<<<26, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
@@ -893,6 +913,8 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
     s.ms_map = ev_ms(c->ev[0], c->ev[1]);
     if (c->T) {
         s.emit_ms = ev_ms(c->ev_emit[0], c->ev_emit[1]);
+        s.resolve_ms = ev_ms(c->ev_emit[1], c->ev_res[1]);
+        s.resolved_tokens = c->n_pending;
         s.emit_bytes = c->nbytes + 8 * c->T;  // tokenize = B + r*T, r = 8-byte record
     }
     if (c->reduced) {

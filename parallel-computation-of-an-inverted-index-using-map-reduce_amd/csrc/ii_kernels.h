@@ -77,8 +77,18 @@ struct Table {
     uint64_t* counters;
 };
 
-__device__ __forceinline__ uint64_t table_hash(const Table& t, uint64_t key) { return mix64(key ^ t.seed); }
-__device__ __forceinline__ uint64_t hot_home(uint64_t hh) { return hh & (kHotSlots - 1); }
+// Home slot of a key in the hot table: a 32-bit multiply-xorshift hash of the
+// key's two halves (cheap enough for every token).  The big table uses an
+// independent 64-bit mix (big_home), only on the miss path.
+__device__ __forceinline__ uint32_t hot_slot(uint64_t key, uint64_t seed) {
+    uint32_t h = ((uint32_t)(key >> 32) ^ (uint32_t)seed) * 0x9E3779B1u +
+                 ((uint32_t)key ^ (uint32_t)(seed >> 32)) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return h & (uint32_t)(kHotSlots - 1);
+}
+__device__ __forceinline__ uint64_t big_home(const Table& t, uint64_t key) { return mix64(key ^ t.seed) & t.big_mask; }
 
 // CAS-insert key at empty slot s; returns the key now stored there.
 __device__ __forceinline__ unsigned long long table_claim(const Table& t, uint64_t s, uint64_t key, uint64_t pos) {
@@ -96,11 +106,10 @@ __device__ __forceinline__ unsigned long long table_claim(const Table& t, uint64
 // home costs one round trip; the bucket is scanned with bit masks in probe
 // order (home, home+1, ... within the bucket); a full bucket sends the word
 // to the big table (linear probing).
-__device__ __forceinline__ uint32_t table_find(const Table& t, uint64_t key, uint64_t hh, uint64_t pos) {
-    const uint64_t home = hot_home(hh);
-    const uint32_t h7 = (uint32_t)(home & (kBucket - 1));
+__device__ __forceinline__ uint32_t table_find(const Table& t, uint64_t key, uint32_t home, uint64_t pos) {
+    const uint32_t h7 = home & (kBucket - 1);
     const uint64_t bbase = home - h7;
-    uint64_t h = (hh >> 20) & t.big_mask;
+    uint64_t h = big_home(t, key);
     const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(t.keys + bbase);
     const ulonglong2 p0 = bp[0], p1 = bp[1], p2 = bp[2], p3 = bp[3];
     unsigned long long kb = t.keys[kHotSlots + h];
@@ -166,11 +175,11 @@ struct TileReader {
     const uint8_t* s;
     const uint8_t* __restrict__ text;
     uint64_t nbytes, tile_lo;
-    uint32_t di, dw;
-    __device__ __forceinline__ TileReader(const uint8_t* s_, const uint8_t* text_, uint64_t nb, uint64_t lo)
-        : s(s_), text(text_), nbytes(nb), tile_lo(lo), di(0xFFFFFFFFu), dw(0) {}
+    uint32_t lim, di, dw;  // lim = bytes staged in LDS after the 16-byte left piece
+    __device__ __forceinline__ TileReader(const uint8_t* s_, const uint8_t* text_, uint64_t nb, uint64_t lo, uint32_t lim_)
+        : s(s_), text(text_), nbytes(nb), tile_lo(lo), lim(lim_), di(0xFFFFFFFFu), dw(0) {}
     __device__ __forceinline__ uint32_t get(uint32_t j) {
-        if (j < (uint32_t)(kTile + kHalo)) {
+        if (j < lim) {
             const uint32_t a = 16 + j;
             if ((a >> 2) != di) {
                 di = a >> 2;
@@ -327,7 +336,7 @@ __device__ __forceinline__ uint32_t lane_starts(const uint4& v, const Classes& c
 // ends before the token shows a letter, space or NUL.
 __device__ __forceinline__ uint32_t kept_starts(uint32_t starts, const Classes& cl, const uint8_t* s_text,
                                                 const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t tile_lo,
-                                                uint32_t wlo) {
+                                                uint32_t wlo, uint32_t lim = kTile + kHalo) {
     const uint32_t ev = cl.letter | cl.ws | cl.nul;
     uint32_t kept = 0;
     for (uint32_t m = starts & ~cl.letter; m; m &= m - 1) {  // starts that are not letters themselves
@@ -336,7 +345,7 @@ __device__ __forceinline__ uint32_t kept_starts(uint32_t starts, const Classes& 
         bool k;
         if (e) k = (cl.letter >> (i + __builtin_ctz(e))) & 1u;
         else {
-            TileReader rd(s_text, text, nbytes, tile_lo);
+            TileReader rd(s_text, text, nbytes, tile_lo, lim);
             k = token_kept(rd, wlo + 16);
         }
         kept |= (uint32_t)k << i;
@@ -383,19 +392,27 @@ __device__ __forceinline__ bool fast_key(const uint4& tb, TokKey& out) {
     return true;
 }
 
+// 16 bytes of the text at any position g, from two aligned 16-B loads.
+__device__ __forceinline__ uint4 global_block16(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t g) {
+    const int64_t a = (int64_t)(g & ~15ull);
+    const uint4 lo = load16(text, nbytes, a), hi = load16(text, nbytes, a + 16);
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return token_bytes(w, (uint32_t)(g & 15u));
+}
+
 // 16 bytes of the staged tile at tile-local position p (any alignment):
 // two aligned LDS reads + byte shift; past the staged halo, global memory.
 __device__ __forceinline__ uint4 tile_block16(const uint8_t* s_text, const uint8_t* __restrict__ text, uint64_t nbytes,
-                                              uint64_t tile_lo, uint32_t p) {
+                                              uint64_t tile_lo, uint32_t p, uint32_t lim) {
     const uint32_t a = 16 + p;
     const uint32_t base = a & ~15u;
-    if (base + 32 <= (uint32_t)(16 + kTile + kHalo)) {
+    if (base + 32 <= 16 + lim) {
         const uint4 lo = *reinterpret_cast<const uint4*>(s_text + base);
         const uint4 hi = *reinterpret_cast<const uint4*>(s_text + base + 16);
         const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         return token_bytes(w, a & 15u);
     }
-    return load16(text, nbytes, (int64_t)tile_lo + p);
+    return global_block16(text, nbytes, tile_lo + p);
 }
 
 __device__ __forceinline__ uint32_t byte_dyn(const uint4& b, uint32_t j) {
@@ -406,7 +423,7 @@ __device__ __forceinline__ uint32_t byte_dyn(const uint4& b, uint32_t j) {
 // SWAR classes, then only the letter bytes are visited.  Stops at whitespace,
 // NUL or the 299th letter.  first16 = the token's first 16 bytes.
 __device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, const uint8_t* __restrict__ text,
-                                              uint64_t nbytes, uint64_t tile_lo, uint32_t p, uint64_t seed) {
+                                              uint64_t nbytes, uint64_t tile_lo, uint32_t p, uint64_t seed, uint32_t lim) {
     uint64_t packed = 0, hash = 1469598103934665603ull;
     uint32_t n = 0, first = 0;
     for (;;) {
@@ -427,7 +444,7 @@ __device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, co
         }
         if (done) break;
         p += 16;
-        b = tile_block16(s_text, text, nbytes, tile_lo, p);
+        b = tile_block16(s_text, text, nbytes, tile_lo, p, lim);
     }
     return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
 }
@@ -463,196 +480,353 @@ struct LongTok {
 };
 constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 
-// Queue a long token for k_long_verify: into the workgroup's LDS buffer, or
-// straight to global memory when the tile alone overflows the buffer.
-__device__ __forceinline__ void queue_long(bool direct, LongTok* s_long, uint32_t* s_lcount, uint64_t lbase,
-                                           LongTok* __restrict__ longs, uint64_t long_cap, const Table& tab, uint64_t pos,
-                                           uint32_t slot) {
-    if (direct) {
-        const uint64_t li = lbase + atomicAdd(s_lcount, 1u);
-        if (li < long_cap) longs[li] = LongTok{pos, slot};
-        else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-    } else {
-        s_long[atomicAdd(s_lcount, 1u)] = LongTok{pos, slot};
+// ---------------------------------------------------------------- K1b emit
+// A workgroup walks its 64 KiB chunk in rounds of 16 KiB: 4 windows of 16 B
+// per lane, window w = 256 j + lane, so each load instruction reads 1 KiB
+// contiguous.  Per round:
+//   1. SWAR classes per window -> kept token starts (main.c:102-113) and the
+//      window's terminator / letter bit masks, kept in LDS;
+//   2. one block scan of 4 packed 16-bit counts -> the token index of every
+//      kept start in text order; the starts are listed in LDS;
+//   3. batches of 1024 tokens, 4 per thread, one token per lane: the register
+//      key path (masks + 12 bytes from LDS, 5-bit packing, main.c:105-111)
+//      and the hot-table home probe with 4 loads in flight per thread; a hit
+//      stores its record straight to HBM (consecutive lanes, consecutive
+//      records);
+//   4. the batch's probe misses and general-path tokens (inner punctuation,
+//      > 12 letters, > 16 bytes) compacted in LDS, one per thread.
+// Records rec[i] = slot << 32 | file id0, in text order (the partial files'
+// "word id" lines, main.c:116).  First letters are counted per chunk
+// (chunk_hist = the partial_<letter>.txt line counts); tokens of > 12 letters
+// are queued for the hash-collision check.
+constexpr int kWin = 4;                          // 16-B windows per lane per round
+constexpr int kRound = kWin * 16 * kBlock;       // 16 KiB of text per round
+constexpr int kRoundWins = kRound / 16;          // windows per round
+constexpr int kRoundStaged = kRound + kHalo;     // bytes staged in LDS after the left piece
+constexpr int kMaxRoundTok = kRound / 2;         // a token start needs a space before it
+static_assert(kChunk % kRound == 0, "a chunk is a whole number of rounds");
+static_assert(kWin * 16 <= 64, "4 packed 16-bit window counts per lane");
+
+struct RoundRegs {
+    uint4 v[kWin];  // lane's windows
+    uint4 h;        // left piece (lane 0) / halo pieces (lanes 1..32)
+};
+__device__ __forceinline__ void fetch_round(RoundRegs& r, const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t lo) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kWin; j++) r.v[j] = load16(text, nbytes, (int64_t)lo + 16 * (kBlock * j + t));
+    r.h = make_uint4(0, 0, 0, 0);
+    if (t < kExtraPieces) r.h = load16(text, nbytes, (int64_t)lo + 16 * (t == 0 ? -1 : kRoundWins + t - 1));
+}
+__device__ __forceinline__ void store_round(uint8_t* s_text, const RoundRegs& r) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kWin; j++) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (kBlock * j + t)) = r.v[j];
+    if (t < kExtraPieces) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (t == 0 ? -1 : kRoundWins + t - 1)) = r.h;
+}
+
+// 4 letters (bytes, first in the low byte) -> their 5-bit codes, first letter
+// in the high bits (20 bits).  x & 0x1F is the letter code for A-Z and a-z.
+__device__ __forceinline__ uint32_t pack4(uint32_t x) {
+    uint32_t r = __builtin_bswap32(x & 0x1F1F1F1Fu);            // b0@24 b1@16 b2@8 b3@0
+    r = (r & 0x001F001Fu) | ((r >> 3) & 0x03E003E0u);           // b0@21 b1@16 b2@5 b3@0
+    return (r & 0x3FFu) | ((r >> 6) & 0xFFC00u);                // b0@15 b1@10 b2@5 b3@0
+}
+
+// Register key path of the cleaning loop (main.c:105-111) for the common
+// token: its letters form one run from its first byte, at most 12 of them,
+// ended by whitespace / NUL (trailing punctuation allowed).  The masks come
+// from the round's window masks, the letters are 12 bytes read from LDS.
+// Returns false for every other token (general path).
+__device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint32_t* s_mask, uint32_t p, TokKey& k) {
+    const uint32_t w0 = p >> 4, sh = p & 15u;
+    const uint32_t m0 = s_mask[w0], m1 = s_mask[w0 + 1];
+    const uint32_t term = ((m0 & 0xFFFFu) | (m1 << 16)) >> sh;
+    const uint32_t let = ((m0 >> 16) | (m1 & 0xFFFF0000u)) >> sh;
+    if (term == 0) return false;
+    const uint32_t e = __builtin_ctz(term);
+    const uint32_t lm = let & ((1u << e) - 1u);
+    const uint32_t n = __popc(lm);
+    if (n == 0 || n > 12 || lm != (1u << n) - 1u) return false;
+    const uint32_t a = 16u + p, al = a & 3u;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_text) + (a >> 2);
+    const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2], d3 = s32[3];
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, al);
+    const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, al);
+    const uint32_t x2 = __builtin_amdgcn_alignbyte(d3, d2, al);
+    const uint64_t key = ((uint64_t)pack4(x0) << 44) | ((uint64_t)pack4(x1) << 24) | ((uint64_t)pack4(x2) << 4);
+    k.key = key & (~0ull << (64 - 5 * n));
+    k.nlet = n;
+    k.first = (x0 & 31u) - 1u;
+    return true;
+}
+
+// Index of this lane's entry when the lanes with `want` append one entry each
+// to an LDS list: one LDS atomic per wave.  Call from wave-uniform control flow.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return 0;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(m & lanemask_lt());
+}
+
+// Fast-path lookup of K1b from the match / occupied bit masks of the key's
+// 8-slot hot bucket: the slot holding the key; for a new word, the bucket's
+// first empty slot in probe order, claimed (table_find's rule, so a word
+// still lives in exactly one place); kSlotNone when the word takes the
+// resolve path (full bucket: the word is, or goes, in the big table; or the
+// claim raced).
+__device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t match, uint32_t full, uint64_t key,
+                                                   uint32_t home, uint64_t pos) {
+    const uint32_t h7 = home & (kBucket - 1);
+    const uint32_t bbase = home - h7;
+    if (match) return bbase + __builtin_ctz(match);
+    const uint32_t empty = ~full & 0xFFu;
+    if (!empty) return kSlotNone;
+    const uint32_t rot = ((empty >> h7) | (empty << (8 - h7))) & 0xFFu;
+    const uint32_t p = (h7 + __builtin_ctz(rot)) & (kBucket - 1);
+    return table_claim(t, bbase + p, key, pos) == key ? bbase + p : kSlotNone;
+}
+
+// 4 bits -> the even bits of a byte
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {
+    x = (x | (x << 2)) & 0x33u;
+    return (x | (x << 1)) & 0x55u;
+}
+
+// Cooperative hot-bucket probe: every lane holds one token (key, home, fast);
+// the wave probes its 64 tokens' buckets in 4 rounds of 16, 4 lanes per
+// bucket each loading one 16-B quarter, so a bucket costs one cache line
+// access per instruction (a lane-private 64-B probe would cost four).  The
+// owner lane gets its bucket's 8-bit match / occupied masks.
+__device__ __forceinline__ void wave_bucket_probe(const Table& t, uint64_t key, uint32_t home, uint64_t fastmask,
+                                                  uint32_t& match, uint32_t& full) {
+    const int l = lane_id();
+    const uint32_t quarter = 2u * (l & 3);
+    ulonglong2 part[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int src = 16 * r + (l >> 2);
+        const uint32_t h = (uint32_t)__shfl((int)home, src, 64);
+        part[r] = make_ulonglong2(0ull, 0ull);
+        if ((fastmask >> src) & 1ull)
+            part[r] = *reinterpret_cast<const ulonglong2*>(t.keys + (h & ~(uint32_t)(kBucket - 1)) + quarter);
+    }
+    match = full = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int src = 16 * r + (l >> 2);
+        const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), src, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)key, src, 64);
+        const uint64_t m0 = __ballot(part[r].x == k), m1 = __ballot(part[r].y == k);
+        const uint64_t f0 = __ballot(part[r].x != 0ull), f1 = __ballot(part[r].y != 0ull);
+        if ((l >> 4) == r) {
+            const int b = 4 * (l & 15);
+            match = spread4((uint32_t)(m0 >> b) & 0xFu) | (spread4((uint32_t)(m1 >> b) & 0xFu) << 1);
+            full = spread4((uint32_t)(f0 >> b) & 0xFu) | (spread4((uint32_t)(f1 >> b) & 0xFu) << 1);
+        }
     }
 }
 
-// K1b: chunk_off holds exclusive record offsets.  Per 4 KiB tile:
-//   1. masks -> kept token starts, block scan -> token index per lane
-//   2. each lane walks its kept tokens (LDS) -> word key into s_key[index]
-//   3. the tile's tokens are spread evenly over the 256 threads, which probe
-//      the word table with up to 4 independent loads in flight each
-//   4. records rec[i] = slot << 32 | file id0 leave through LDS, coalesced.
-// First letters are counted per chunk (chunk_hist[chunk][26] = the
-// partial_<letter>.txt line counts); tokens of > 12 letters are queued for the
-// hash-collision check.  No global atomics on a shared word per token.
+// Unresolved token of a chunk (K1b -> K1c), one u32: chunk-relative start
+// (16 bits) | chunk-relative token index << 16 (15 bits) | general path << 31.
+// A fast-path miss leaves its key in its record slot.
+constexpr uint32_t kPendSlow = 1u << 31;
+
+// Letter histogram update without same-address LDS atomics inside a wave:
+// lanes are matched on their 5-bit letter (5 ballots) and the lowest lane of
+// each group adds the group's size.  Call from wave-uniform control flow.
+__device__ __forceinline__ void wave_hist_add(uint32_t* hist, uint32_t letter, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+        const bool bit = (letter >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[letter], (uint32_t)__popcll(m));
+}
+
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
-// bit 0 = skip the table probe, bit 1 = skip the token walk, bit 2 = skip the
-// letter histogram, bit 3 = no long-token queue, bit 4 = fast path only.
+// bit 0 = skip the table probe, bit 2 = skip the letter histogram.
 template <int kAblate = 0>
 __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                      const uint64_t* __restrict__ file_start,
                                                      const uint32_t* __restrict__ file_id, uint32_t nfiles,
                                                      const uint64_t* __restrict__ chunk_off, Table tab,
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                     LongTok* __restrict__ longs, uint64_t long_cap) {
-    constexpr int kMaxTok = kTile / 2 + 1;
-    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
-    __shared__ uint64_t s_key[kMaxTok];   // word key, then the record
-    __shared__ uint16_t s_off[kMaxTok];   // tile offset | 0x8000 if long
-    __shared__ uint16_t s_slow[kMaxTok];  // tokens for the general key path
-    __shared__ uint32_t s_nslow, s_nmiss;
-    __shared__ LongTok s_long[kLongBuf];
+                                                     uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kRoundStaged];
+    __shared__ uint32_t s_mask[kRoundWins + 1];   // per window: terminator (ws | NUL) bits | letter bits << 16
+    __shared__ uint16_t s_off[kMaxRoundTok];      // round-local start of every kept token, text order
     __shared__ uint64_t s_scan[kWaves + 1];
     __shared__ uint32_t s_hist[32];
-    __shared__ uint32_t s_f[2];
-    __shared__ uint32_t s_lcount;
-    __shared__ uint64_t s_lbase;
+    __shared__ uint32_t s_f[3];                   // first / last file of the chunk, id0 of the first
+    __shared__ uint32_t s_npend;
 
+    const int t = threadIdx.x;
     const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
-    const int t = threadIdx.x;
     if (t < 32) s_hist[t] = 0;
     if (t == 0) {
         s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
         s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
-        s_lcount = 0;
+        s_f[2] = file_id[s_f[0]];
+        s_npend = 0;
     }
-    uint64_t out = chunk_off[blockIdx.x];
-    const uint32_t wlo = (uint32_t)t * 16;
-
-    TileRegs nxt = fetch_tile(text, nbytes, chunk_lo);
-    for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
+    const uint64_t cbase = chunk_off[blockIdx.x];
+    uint64_t out = cbase;
+    RoundRegs nxt;
+    fetch_round(nxt, text, nbytes, chunk_lo);
+    for (uint64_t lo = chunk_lo; lo < chunk_hi; lo += kRound) {
+        __syncthreads();  // the previous round's readers of s_text / s_off are done
+        store_round(s_text, nxt);
+        const RoundRegs cur = nxt;
+        if (lo + kRound < chunk_hi) fetch_round(nxt, text, nbytes, lo + kRound);
         __syncthreads();
-        store_tile(s_text, nxt);
-        const uint4 v = nxt.v;
-        if (tile_lo + kTile < chunk_hi) nxt = fetch_tile(text, nbytes, tile_lo + kTile);
-        __syncthreads();
-        // 1. kept starts
-        if (t == 0) s_nslow = s_nmiss = 0;
-        const Classes cl = classify16(v);
-        const uint32_t kept = kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo);
+        // 1. kept starts and window masks
+        uint32_t kept[kWin];
+        uint64_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < kWin; j++) {
+            const uint32_t w = kBlock * j + t;
+            const Classes cl = classify16(cur.v[j]);
+            s_mask[w] = (cl.ws | cl.nul) | (cl.letter << 16);
+            uint32_t prev = __shfl_up(cur.v[j].w, 1, 64) >> 24;  // byte before the window
+            if ((t & 63) == 0) prev = s_text[16 + 16 * w - 1];
+            const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
+            kept[j] = kept_starts(starts, cl, s_text, text, nbytes, lo, 16 * w, kRoundStaged);
+            cnt |= (uint64_t)__popc(kept[j]) << (16 * j);
+        }
+        if (t == 1) {  // first halo window: masks past the round's last byte
+            const Classes ch = classify16(cur.h);
+            s_mask[kRoundWins] = (ch.ws | ch.nul) | (ch.letter << 16);
+        }
+        // 2. token index of every kept start (window j of all lanes before j + 1)
         uint64_t tot;
-        uint32_t o = (uint32_t)block_excl_scan(__popc(kept), &tot, s_scan);
-        // 2a. word keys, register fast path; the rest go to a compact list
-        uint32_t nlong = 0;
-        {
-            const uint4 nx = *reinterpret_cast<const uint4*>(s_text + 16 + wlo + 16);  // next lane's window
-            const uint32_t w8[8] = {v.x, v.y, v.z, v.w, nx.x, nx.y, nx.z, nx.w};
-            for (uint32_t m = kept; m; m &= m - 1) {
-                const uint32_t i = __builtin_ctz(m);
-                TokKey k;
-                bool ok;
-                if (kAblate & 2) {
-                    k = TokKey{(uint64_t)(wlo + i + 1) << 8, 3u, i % 26u};
-                    ok = true;
-                } else {
-                    ok = fast_key(token_bytes(w8, i), k);
-                }
-                s_off[o] = (uint16_t)(wlo + i);
-                if (ok) {
-                    if (!(kAblate & 4)) atomicAdd(&s_hist[k.first], 1u);
-                    s_key[o] = k.key;
-                } else {
-                    s_slow[atomicAdd(&s_nslow, 1u)] = (uint16_t)o;
-                }
-                o++;
-            }
+        const uint64_t ex = block_excl_scan(cnt, &tot, s_scan);
+        uint32_t ntok = 0;
+#pragma unroll
+        for (int j = 0; j < kWin; j++) {
+            uint32_t o = ntok + (uint32_t)((ex >> (16 * j)) & 0xFFFFu);
+            const uint32_t wlo = 16 * (kBlock * j + t);
+            for (uint32_t m = kept[j]; m; m &= m - 1) s_off[o++] = (uint16_t)(wlo + __builtin_ctz(m));
+            ntok += (uint32_t)((tot >> (16 * j)) & 0xFFFFu);
         }
         __syncthreads();
-        // 2b. general path (inner punctuation, > 12 letters, > 16 bytes), one token per thread
-        for (uint32_t q = t; q < s_nslow; q += kBlock) {
-            const uint32_t j = s_slow[q];
-            const uint32_t p = s_off[j];
-            TokKey k = (kAblate & 16) ? TokKey{(uint64_t)(p + 1) << 8, 3u, p % 26u}
-                                      : general_key(tile_block16(s_text, text, nbytes, tile_lo, p), s_text, text, nbytes,
-                                                    tile_lo, p, tab.seed);
-            if (kAblate & 8) k.nlet = k.nlet > 12 ? 12 : k.nlet;
-            if (!(kAblate & 4)) atomicAdd(&s_hist[k.first], 1u);
-            s_key[j] = k.key;
-            if (k.nlet > 12) {
-                s_off[j] = (uint16_t)(p | 0x8000u);
-                nlong++;
+        const bool fsame = s_f[0] == s_f[1];
+        const uint32_t fid0 = s_f[2];
+        const uint32_t qbase = (uint32_t)(out - cbase), pbase = (uint32_t)(lo - chunk_lo);
+        // 3. keys + cooperative hot-bucket probes, one token per lane; no barrier
+        for (uint32_t b0 = 0; b0 < ntok; b0 += kBlock) {
+            const uint32_t q = b0 + t;
+            const bool valid = q < ntok;
+            const uint32_t p = valid ? s_off[q] : 0u;
+            TokKey k{0ull, 0u, 0u};
+            const bool fast = valid && round_fast_key(s_text, s_mask, p, k);
+            const uint32_t home = hot_slot(k.key, tab.seed);
+            if (!(kAblate & 4)) wave_hist_add(s_hist, k.first, fast);
+            uint32_t slot = kSlotNone;
+            if (kAblate & 1) {
+                if (fast) slot = home;
+            } else {
+                uint32_t match, full;
+                wave_bucket_probe(tab, k.key, home, __ballot(fast), match, full);
+                if (fast) slot = bucket_resolve(tab, match, full, k.key, home, lo + p);
             }
+            const bool resolved = fast && slot != kSlotNone;
+            if (resolved) {
+                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, s_f[0], s_f[1], lo + p)];
+                rec[out + q] = ((uint64_t)slot << 32) | f;
+            } else if (fast) {
+                rec[out + q] = k.key;
+            }
+            const bool pending = valid && !resolved;
+            const uint32_t pi = wave_append(&s_npend, pending);
+            if (pending) pend[cbase + pi] = (pbase + p) | ((qbase + q) << 16) | (fast ? 0u : kPendSlow);
         }
-        uint64_t ltot;
-        (void)block_excl_scan(nlong, &ltot, s_scan);  // also the barrier before phase 3
-        // long-token queue: LDS buffer, one global atomic per flush
-        const bool direct = ltot > (uint64_t)kLongBuf;
-        if (ltot && (direct || s_lcount + ltot > (uint64_t)kLongBuf)) {
-            if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)s_lcount);
-            __syncthreads();
-            for (uint32_t q = t; q < s_lcount; q += kBlock) {
-                if (s_lbase + q < long_cap) longs[s_lbase + q] = s_long[q];
-                else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-            }
-            __syncthreads();
-            if (t == 0) {
-                s_lcount = 0;
-                if (direct) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)ltot);
-            }
-            __syncthreads();
-        }
-        // 3a. probe the hot-table home slot: token q = t + u*kBlock, four
-        //     loads in flight per thread; misses go to a compact list
-        const uint32_t ntok = (uint32_t)tot;
-        const uint32_t fsame = s_f[0] == s_f[1];
-        for (uint32_t base = t; base < ntok; base += 4 * kBlock) {
-            uint64_t key[4], h[4];
-            unsigned long long kk[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t q = base + u * kBlock;
-                key[u] = q < ntok ? s_key[q] : 0ull;
-                h[u] = table_hash(tab, key[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                kk[u] = (kAblate & 1) ? key[u] : (base + u * kBlock < ntok) ? tab.keys[hot_home(h[u])] : 0ull;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t q = base + u * kBlock;
-                if (q >= ntok) continue;
-                if (kk[u] != key[u]) {
-                    s_slow[atomicAdd(&s_nmiss, 1u)] = (uint16_t)q;
-                    continue;
-                }
-                const uint32_t off = s_off[q];
-                const uint64_t pos = tile_lo + (off & 0x7FFFu);
-                const uint32_t slot = (uint32_t)hot_home(h[u]);
-                const uint32_t f = fsame ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
-                s_key[q] = ((uint64_t)slot << 32) | file_id[f];
-                if (off & 0x8000u) queue_long(direct, s_long, &s_lcount, s_lbase, longs, long_cap, tab, pos, slot);
-            }
-        }
-        __syncthreads();
-        // 3b. misses, one per thread: bucket line + big-table home in one round trip
-        for (uint32_t r = t; r < s_nmiss; r += kBlock) {
-            const uint32_t q = s_slow[r];
-            const uint64_t key = s_key[q];
-            const uint32_t off = s_off[q];
-            const uint64_t pos = tile_lo + (off & 0x7FFFu);
-            const uint32_t slot = table_find(tab, key, table_hash(tab, key), pos);
-            const uint32_t f = fsame ? s_f[0] : file_of(file_start, s_f[0], s_f[1], pos);
-            s_key[q] = ((uint64_t)slot << 32) | file_id[f];
-            if (off & 0x8000u) queue_long(direct, s_long, &s_lcount, s_lbase, longs, long_cap, tab, pos, slot);
-        }
-        __syncthreads();
-        if (direct && t == 0) s_lcount = 0;
-        // 4. coalesced record store
-        for (uint32_t q = t; q < ntok; q += kBlock) rec[out + q] = s_key[q];
-        out += tot;
+        out += ntok;
     }
     __syncthreads();
-    if (s_lcount) {
-        if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)s_lcount);
+    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
+    if (t == 0) pend_cnt[blockIdx.x] = s_npend;
+}
+
+// K1c: the tokens K1b left unresolved, one per thread across the chunk —
+// general-path tokens (main.c:105-111 with inner punctuation, > 12 letters or
+// > 16 bytes: key from the text in HBM) and words whose hot bucket is full or
+// whose claim raced — full table lookup / insert (table_find), record.  Many
+// independent lookups in flight instead of a barrier-bound phase inside K1b.
+__global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                        const uint64_t* __restrict__ file_start,
+                                                        const uint32_t* __restrict__ file_id, uint32_t nfiles,
+                                                        const uint64_t* __restrict__ chunk_off,
+                                                        const uint32_t* __restrict__ pend,
+                                                        const uint32_t* __restrict__ pend_cnt, Table tab,
+                                                        uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
+                                                        LongTok* __restrict__ longs, uint64_t long_cap) {
+    __shared__ LongTok s_long[kLongBuf];
+    __shared__ uint32_t s_hist[32];
+    __shared__ uint32_t s_f[3];
+    __shared__ uint32_t s_lcount;
+    __shared__ uint64_t s_lbase;
+    const uint32_t n = pend_cnt[blockIdx.x];
+    if (n == 0) return;
+    const int t = threadIdx.x;
+    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
+    if (t < 32) s_hist[t] = 0;
+    if (t == 0) {
+        s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
+        s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
+        s_f[2] = file_id[s_f[0]];
+        s_lcount = 0;
+    }
+    __syncthreads();
+    const uint64_t cbase = chunk_off[blockIdx.x];
+    const bool fsame = s_f[0] == s_f[1];
+    for (uint32_t i = t; i < n; i += kBlock) {
+        const uint32_t e = pend[cbase + i];
+        const uint64_t pos = chunk_lo + (e & 0xFFFFu);
+        const uint64_t r = cbase + ((e >> 16) & 0x7FFFu);
+        uint64_t key;
+        uint32_t nlet = 0;
+        if (e & kPendSlow) {
+            const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
+            atomicAdd(&s_hist[k.first], 1u);
+            key = k.key;
+            nlet = k.nlet;
+        } else {
+            key = rec[r];
+        }
+        const uint32_t slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
+        const uint32_t f = fsame ? s_f[2] : file_id[file_of(file_start, s_f[0], s_f[1], pos)];
+        rec[r] = ((uint64_t)slot << 32) | f;
+        if (nlet > 12) {  // hashed key: queue for the exactness check
+            const uint32_t li = atomicAdd(&s_lcount, 1u);
+            if (li < (uint32_t)kLongBuf) {
+                s_long[li] = LongTok{pos, slot};
+            } else {  // the chunk alone overflows the buffer: straight to the global queue
+                const uint64_t g = atomicAdd((unsigned long long*)&tab.counters[C_LONG], 1ull);
+                if (g < long_cap) longs[g] = LongTok{pos, slot};
+                else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+            }
+        }
+    }
+    __syncthreads();
+    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] += s_hist[t];
+    const uint32_t nl = s_lcount < (uint32_t)kLongBuf ? s_lcount : (uint32_t)kLongBuf;
+    if (nl) {
+        if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)nl);
         __syncthreads();
-        for (uint32_t q = t; q < s_lcount; q += kBlock) {
+        for (uint32_t q = t; q < nl; q += kBlock) {
             if (s_lbase + q < long_cap) longs[s_lbase + q] = s_long[q];
             else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
         }
     }
-    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
