@@ -82,6 +82,8 @@ typedef struct {
     uint64_t emit_bytes;   /* its algorithmic bytes: B text read + 8 B per record written */
     double resolve_ms;     /* K1c k_tok_resolve (tokens the emit kernel left unresolved) */
     uint64_t resolved_tokens; /* tokens K1b handed to K1c (general path, full hot bucket, raced claim) */
+    double sort0_ms;       /* first token-sort pass: dedup + lexid remap + compaction (k_sort0_compact) */
+    uint64_t sort0_bytes;  /* its algorithmic bytes: 8 B per record read + 8 B per kept record written */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

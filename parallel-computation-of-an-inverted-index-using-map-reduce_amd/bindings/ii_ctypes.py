@@ -36,6 +36,7 @@ class Stats(ctypes.Structure):
         ("scatter_launches", ctypes.c_uint32), ("sorted_records", ctypes.c_uint64),
         ("emit_ms", ctypes.c_double), ("emit_bytes", ctypes.c_uint64), ("resolve_ms", ctypes.c_double),
         ("resolved_tokens", ctypes.c_uint64),
+        ("sort0_ms", ctypes.c_double), ("sort0_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -40,7 +40,7 @@ struct ii_ctx {
     DBuf fstart, fid;
 
     // scratch
-    DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable;
+    DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable, kept;
     // K1
     DBuf rec, rec2, longs, pend, pend_cnt;
     DBuf tkeys, trep;
@@ -74,6 +74,8 @@ struct ii_ctx {
     uint64_t sc_bytes[kMaxTimedPasses] = {0};  // algorithmic bytes of each timed scatter launch
     int n_sc = 0;
     uint64_t T_sorted = 0;  // records left after the pass-0 dedup
+    hipEvent_t ev_c0[2] = {};  // around k_sort0_compact
+    uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
     uint64_t n_pending = 0; // tokens K1b left to K1c
     ii_stats stats;
 };
@@ -176,59 +178,78 @@ struct OpInPlace {
 
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
-// With dedup0 (token sort only) the first pass also drops repeated
-// (hot word, file) records; *n_out receives the number of records kept.
+// With remap0 (token sort only, no values) the first pass is k_sort0_compact:
+// it drops repeated (hot word, file) records, maps slots to lexicographic ids
+// and compacts each workgroup's range into *k2; that pass's scatter reads the
+// kept ranges back into *k, and the remaining passes run over the kept
+// records only.  *n_out receives the number of records kept.
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
-                    bool timed, int* passes, const uint32_t* remap0 = nullptr, bool dedup0 = false,
-                    uint64_t* n_out = nullptr) {
+                    bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr) {
     if (passes) *passes = 0;
     if (n_out) *n_out = n;
     if (n <= 1 || hi <= lo) return II_OK;
-    uint64_t n_kept = n;  // records surviving the pass-0 dedup
-    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
-    uint64_t chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
-    nch = (n + chunk - 1) / chunk;
-    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * nch));
+    if (remap0 && v) return II_ERR_INTERNAL;
+    uint64_t nch = 0, chunk = 0;
+    auto regrid = [&](uint64_t m) {
+        nch = std::min<uint64_t>(kMaxChunks, (m + kSortTile - 1) / kSortTile);
+        chunk = ((m + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
+        nch = (m + chunk - 1) / chunk;
+    };
+    regrid(n);
+    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
+    CK(grow(c->kept, sizeof(uint64_t) * kMaxChunks));
     uint64_t* table = P_<uint64_t>(c->rtable);
+    uint64_t* kept = P_<uint64_t>(c->kept);
     const bool kv = v != nullptr;
     uint64_t* totals = P_<uint64_t>(c->totals);
-    for (int shift = lo; shift < hi; shift += kRadixBits) {
-        const uint32_t* remap = shift == lo ? remap0 : nullptr;
-        const bool dd = dedup0 && shift == lo;
-        if (shift != lo && n != n_kept) {  // records were dropped: regrid the remaining passes
-            n = n_kept;
-            if (n <= 1) break;
-            nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
-            chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
-            nch = (n + chunk - 1) / chunk;
-        }
-        if (dd) k_radix_hist<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
-        else k_radix_hist<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, (uint32_t)nch, table, remap);
-        CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, dd ? totals + 4 : nullptr));
+    // even digit widths: the fewest passes of <= kRadixBits bits, each as narrow
+    // as that allows (fewer buckets -> longer output runs per tile)
+    const int npass = (hi - lo + kRadixBits - 1) / kRadixBits;
+    const int bits = (hi - lo + npass - 1) / npass;
+    for (int shift = lo; shift < hi; shift += bits) {
+        const int db = std::min(bits, hi - shift);
+        const uint32_t dmask = (1u << db) - 1u;
+        const bool first0 = remap0 && shift == lo;
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
+        if (first0) {
+            if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
+            k_sort0_compact<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table, remap0,
+                                                                 *k2, kept);
+            if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
+            CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
+        } else {
+            k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table);
+            CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
+        }
         if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        const uint64_t n_in = n;
+        const uint64_t* src = first0 ? *k2 : *k;
+        uint64_t* dst = first0 ? *k : *k2;
         if (kv)
-            k_radix_scatter<true, false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, *v, *v2, n, chunk, shift,
-                                                                              (uint32_t)nch, table, remap);
-        else if (dd)
-            k_radix_scatter<false, true><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
-                                                                              (uint32_t)nch, table, remap);
+            k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, *v, *v2, n, chunk, shift, db,
+                                                                      (uint32_t)nch, table, nullptr);
         else
-            k_radix_scatter<false, false><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift,
-                                                                               (uint32_t)nch, table, remap);
+            k_radix_scatter<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, nullptr, nullptr, n, chunk, shift, db,
+                                                                       (uint32_t)nch, table, first0 ? kept : nullptr);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
             c->n_sc++;
         }
         HIPCK(hipGetLastError());
-        std::swap(*k, *k2);
-        if (kv) std::swap(*v, *v2);
         if (passes) (*passes)++;
-        if (dd) CK(read_u64(c, totals + 4, &n_kept));
-        if (ev) c->sc_bytes[c->n_sc - 1] = 8 * n_in + 8 * (dd ? n_kept : n_in) + (kv ? 8 * n_in : 0);
+        if (first0) {  // sorted by the first digit, in *k: the rest runs over the kept records
+            const uint64_t n_in = n;
+            CK(read_u64(c, totals + 4, &n));
+            c->c0_bytes = 8 * n_in + 8 * n;
+            if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n;
+            if (n_out) *n_out = n;
+            if (n <= 1) break;
+            regrid(n);
+        } else {
+            std::swap(*k, *k2);
+            if (kv) std::swap(*v, *v2);
+            if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n + (kv ? 8 * n : 0);
+        }
     }
-    if (n_out) *n_out = n_kept;
     return II_OK;
 }
 
@@ -250,6 +271,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
+    for (auto& e : c->ev_c0) HIPCK(hipEventCreate(&e));
     if (grow(c->partial, sizeof(uint64_t) * (kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
@@ -272,7 +294,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
-                   &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt};
+                   &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -282,6 +304,8 @@ extern "C" void ii_close(ii_ctx* c) {
     for (auto& e : c->ev_emit)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_res)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_c0)
         if (e) (void)hipEventDestroy(e);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
@@ -308,6 +332,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
     c->planned_parts = 0;
     c->host_valid = false;
     c->n_sc = 0;
+    c->c0_bytes = 0;
     c->retries = 0;
     memset(&c->stats, 0, sizeof(c->stats));
     uint64_t* counters = P_<uint64_t>(c->counters);
@@ -629,7 +654,7 @@ static int local_reduce(ii_ctx* c) {
         HIPCK(hipGetLastError());
     }
     uint64_t Tk = T;
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap), true, &Tk));
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap), &Tk));
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
@@ -937,6 +962,10 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.scatter_ms_avg = c->n_sc ? sum / c->n_sc : 0;
         s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: 8 B read per record in, 8 B written per record out
         s.sorted_records = c->T_sorted;
+        if (c->c0_bytes) {
+            s.sort0_ms = ev_ms(c->ev_c0[0], c->ev_c0[1]);
+            s.sort0_bytes = c->c0_bytes;
+        }
     }
     *o = s;
     return II_OK;

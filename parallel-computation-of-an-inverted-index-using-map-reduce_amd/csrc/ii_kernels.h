@@ -65,7 +65,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 //              bucket was already full.
 // A word lives in exactly one place: a probe scans the same bucket (then the
 // same big-table run) in the same order and slots only go empty -> full.
-constexpr int kHotLog2 = 17;
+constexpr int kHotLog2 = 19;
 constexpr uint64_t kHotSlots = 1ull << kHotLog2;
 constexpr int kBucket = 8;
 
@@ -449,28 +449,31 @@ __device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, co
     return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
 }
 
-// K1a: kept tokens per 64 KiB chunk -> chunk_cnt[blockIdx.x].
+// K1a: kept tokens per 64 KiB chunk -> chunk_cnt[blockIdx.x], straight from
+// HBM (no LDS staging): lane t classifies windows w = 256 j + t of the chunk
+// with 16-B loads; the byte before a window comes from the neighbour lane, or
+// a 1-byte load for lane 0 of a wave; the rare start whose keep decision lies
+// past its window walks the text in HBM (kept_starts with nothing staged).
 __global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                       uint64_t* __restrict__ chunk_cnt) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kTile + kHalo];
     __shared__ uint64_t s_scan[kWaves + 1];
+    constexpr int kWinsPerLane = (int)(kChunk / 16 / kBlock);
     const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
-    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
-    const uint32_t wlo = (uint32_t)threadIdx.x * 16;
+    const int t = threadIdx.x;
     uint64_t kept = 0;
-    TileRegs nxt = fetch_tile(text, nbytes, chunk_lo);
-    for (uint64_t tile_lo = chunk_lo; tile_lo < chunk_hi; tile_lo += kTile) {
-        __syncthreads();
-        store_tile(s_text, nxt);
-        const uint4 v = nxt.v;
-        if (tile_lo + kTile < chunk_hi) nxt = fetch_tile(text, nbytes, tile_lo + kTile);
-        __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kWinsPerLane; j++) {
+        const uint64_t g = chunk_lo + 16 * ((uint64_t)kBlock * j + t);
+        const uint4 v = load16(text, nbytes, (int64_t)g);
         const Classes cl = classify16(v);
-        kept += __popc(kept_starts(lane_starts(v, cl, s_text), cl, s_text, text, nbytes, tile_lo, wlo));
+        uint32_t prev = (uint32_t)__shfl_up((int)v.w, 1, 64) >> 24;
+        if ((t & 63) == 0) prev = (g > 0 && g - 1 < nbytes) ? text[g - 1] : 32u;
+        const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
+        kept += __popc(kept_starts(starts, cl, nullptr, text, nbytes, g, 0, 0));
     }
     uint64_t tot;
     (void)block_excl_scan(kept, &tot, s_scan);
-    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = tot;
+    if (t == 0) chunk_cnt[blockIdx.x] = tot;
 }
 
 // Long token queued for the exactness check (k_long_verify).
@@ -650,6 +653,33 @@ __device__ __forceinline__ void wave_hist_add(uint32_t* hist, uint32_t letter, b
     if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[letter], (uint32_t)__popcll(m));
 }
 
+// First-letter counts of the tokens one lane keys in a chunk: 8 bits per
+// letter in 7 registers (a lane keys at most kMaxRoundTok / kBlock = 32 tokens
+// per round, 128 per chunk), updated without LDS traffic; flushed once per
+// chunk as 14 wave sums of two 16-bit fields each.
+__device__ __forceinline__ void lane_hist_add(uint32_t (&lc)[7], uint32_t letter, bool valid) {
+    const uint32_t inc = valid ? 1u << ((letter & 3u) * 8) : 0u;
+    const uint32_t wi = letter >> 2;
+#pragma unroll
+    for (int i = 0; i < 7; i++) lc[i] += wi == (uint32_t)i ? inc : 0u;
+}
+__device__ __forceinline__ void lane_hist_flush(const uint32_t (&lc)[7], uint32_t* hist) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+#pragma unroll
+        for (int odd = 0; odd < 2; odd++) {
+            uint32_t v = (lc[i] >> (8 * odd)) & 0x00FF00FFu;  // letters 4i + odd, 4i + 2 + odd
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+            if (lane_id() == 0) {
+                const int l0 = 4 * i + odd, l1 = l0 + 2;
+                if (l0 < 26 && (v & 0xFFFFu)) atomicAdd(&hist[l0], v & 0xFFFFu);
+                if (l1 < 26 && (v >> 16)) atomicAdd(&hist[l1], v >> 16);
+            }
+        }
+    }
+}
+
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram.
 template <int kAblate = 0>
@@ -679,30 +709,31 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
     }
     const uint64_t cbase = chunk_off[blockIdx.x];
     uint64_t out = cbase;
+    uint32_t lc[7] = {0, 0, 0, 0, 0, 0, 0};
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
     for (uint64_t lo = chunk_lo; lo < chunk_hi; lo += kRound) {
         __syncthreads();  // the previous round's readers of s_text / s_off are done
         store_round(s_text, nxt);
-        const RoundRegs cur = nxt;
         if (lo + kRound < chunk_hi) fetch_round(nxt, text, nbytes, lo + kRound);
         __syncthreads();
-        // 1. kept starts and window masks
+        // 1. kept starts and window masks (windows re-read from LDS: the next
+        //    round's bytes are already in flight in registers)
         uint32_t kept[kWin];
         uint64_t cnt = 0;
 #pragma unroll
         for (int j = 0; j < kWin; j++) {
             const uint32_t w = kBlock * j + t;
-            const Classes cl = classify16(cur.v[j]);
+            const uint4 v = *reinterpret_cast<const uint4*>(s_text + 16 + 16 * w);
+            const Classes cl = classify16(v);
             s_mask[w] = (cl.ws | cl.nul) | (cl.letter << 16);
-            uint32_t prev = __shfl_up(cur.v[j].w, 1, 64) >> 24;  // byte before the window
-            if ((t & 63) == 0) prev = s_text[16 + 16 * w - 1];
+            const uint32_t prev = s_text[16 + 16 * w - 1];  // byte before the window
             const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
             kept[j] = kept_starts(starts, cl, s_text, text, nbytes, lo, 16 * w, kRoundStaged);
             cnt |= (uint64_t)__popc(kept[j]) << (16 * j);
         }
-        if (t == 1) {  // first halo window: masks past the round's last byte
-            const Classes ch = classify16(cur.h);
+        if (t == 0) {  // first halo window: masks past the round's last byte
+            const Classes ch = classify16(*reinterpret_cast<const uint4*>(s_text + 16 + kRound));
             s_mask[kRoundWins] = (ch.ws | ch.nul) | (ch.letter << 16);
         }
         // 2. token index of every kept start (window j of all lanes before j + 1)
@@ -728,7 +759,7 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
             TokKey k{0ull, 0u, 0u};
             const bool fast = valid && round_fast_key(s_text, s_mask, p, k);
             const uint32_t home = hot_slot(k.key, tab.seed);
-            if (!(kAblate & 4)) wave_hist_add(s_hist, k.first, fast);
+            if (!(kAblate & 4)) lane_hist_add(lc, k.first, fast);
             uint32_t slot = kSlotNone;
             if (kAblate & 1) {
                 if (fast) slot = home;
@@ -750,6 +781,7 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
         }
         out += ntok;
     }
+    lane_hist_flush(lc, s_hist);
     __syncthreads();
     if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
     if (t == 0) pend_cnt[blockIdx.x] = s_npend;
@@ -1051,6 +1083,102 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
     int lj = j < V ? (int)(sk[j] >> 59) - 1 : 26;
     int lp = j > 0 ? (int)(sk[j - 1] >> 59) - 1 : -1;
     for (int l = lp + 1; l <= lj; l++) letter_start[l] = j;
+}
+
+// ---------------------------------------------------------------- K2 first pass
+// First pass of the token sort over the records in text order
+// (slot << 32 | file id0), one workgroup per contiguous range, tiles of
+// kSortTile records with the scatter's item mapping:
+//  * drops repeated (hot word, file) records: a record whose slot is a
+//    hot-table slot and whose file is the tile's epoch file is dropped when
+//    the same slot was already kept in this epoch (LDS bitmap, cleared when
+//    the epoch changes; the epoch is the file id0 of each tile's first
+//    record).  Only exact duplicates go, and which copy survives does not
+//    matter, so K3 still sees every distinct (word, file) pair;
+//  * replaces the slot by the word's lexicographic id (remap);
+//  * writes the kept records, in order, to kout[lo ...) and counts their
+//    pass-0 digit (digit-major table, as k_radix_hist).
+// kept[b] = records kept by workgroup b; pass 0's scatter reads
+// [lo, lo + kept[b]) back.
+constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+
+__global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
+                                                          int shift, uint32_t dmask, uint32_t nchunks,
+                                                          uint64_t* __restrict__ table,
+                                                          const uint32_t* __restrict__ remap,
+                                                          uint64_t* __restrict__ kout, uint64_t* __restrict__ kept) {
+    __shared__ uint32_t cnt[kWaves][kRadix];
+    __shared__ uint32_t bm[kDedupWords];
+    __shared__ uint32_t s_wtot[kWaves];
+    __shared__ uint32_t s_epoch, s_flag;
+    const int w = wave_id(), l = lane_id();
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&cnt[0][0])[i] = 0;
+    if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const uint64_t tofs = (uint64_t)w * 64 * kSortItems + l;
+    const uint64_t lt = lanemask_lt();
+    uint64_t o = lo;  // next output position
+    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
+        if (threadIdx.x == 0) {
+            const uint32_t f = (uint32_t)keys[tb];
+            s_flag = f != s_epoch;
+            s_epoch = f;
+        }
+        __syncthreads();
+        if (s_flag) {
+            for (uint32_t i = threadIdx.x; i < kDedupWords; i += kBlock) bm[i] = 0;
+            __syncthreads();
+        }
+        const uint32_t epoch = s_epoch;
+        uint64_t raw[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint64_t idx = tb + tofs + (uint64_t)k * 64;
+            raw[k] = idx < hi ? keys[idx] : 0ull;
+        }
+        uint32_t keep = 0, wcount = 0;
+        uint32_t pos[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            bool ok = tb + tofs + (uint64_t)k * 64 < hi;
+            const uint64_t slot = raw[k] >> 32;
+            if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
+                const uint32_t bit = 1u << (slot & 31);
+                ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
+            }
+            const uint64_t b = __ballot(ok);
+            pos[k] = wcount + (uint32_t)__popcll(b & lt);
+            wcount += (uint32_t)__popcll(b);
+            keep |= (uint32_t)ok << k;
+        }
+        if (l == 0) s_wtot[w] = wcount;
+        __syncthreads();
+        uint32_t wbase = 0, ttot = 0;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ww++) {
+            const uint32_t c = s_wtot[ww];
+            if (ww < w) wbase += c;
+            ttot += c;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            if ((keep >> k) & 1u) {
+                const uint64_t r = ((uint64_t)remap[raw[k] >> 32] << 32) | (raw[k] & 0xFFFFFFFFull);
+                kout[o + wbase + pos[k]] = r;
+                atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
+            }
+        }
+        o += ttot;
+        __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
+    }
+    for (int d = threadIdx.x; d < kRadix; d += kBlock) {
+        uint32_t tt = 0;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ww++) tt += cnt[ww][d];
+        table[(uint64_t)d * nchunks + blockIdx.x] = tt;
+    }
+    if (threadIdx.x == 0) kept[blockIdx.x] = o - lo;
 }
 
 // ---------------------------------------------------------------- K2 support

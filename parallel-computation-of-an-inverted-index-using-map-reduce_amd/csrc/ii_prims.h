@@ -124,77 +124,19 @@ constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortItems = 16;                     // keys per thread per tile
 constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
 
-// Digit extraction functor for a plain key array.
-struct DigitOf {
-    int shift;
-    __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)(k >> shift) & (kRadix - 1); }
-};
-
-// Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
-// one exclusive scan of the table yields every chunk's scatter base).
-// remap (optional, first pass of the token sort): the key's high word is an
-// index into remap, replaced by remap[high word] on load — fuses the
-// slot -> lexicographic-id step into the sort.
-__device__ __forceinline__ uint64_t remap_key(uint64_t k, const uint32_t* __restrict__ remap) {
-    return remap ? (((uint64_t)remap[k >> 32] << 32) | (k & 0xFFFFFFFFull)) : k;
-}
-
-// ---- pass-0 dedup of (word, file) records (token sort only)
-// Records arrive in text order (file ids ascending).  Inside a workgroup's
-// range, a record whose word slot is a hot-table slot (< kDedupSlots) and whose
-// file is the current epoch file is dropped when the same slot was already
-// kept in this epoch (LDS bitmap).  The epoch is the file id of the first
-// record of each 4096-record tile; a change clears the bitmap.  The kept
-// multiset therefore depends only on the data and the tile grid, which the
-// histogram and the scatter share, so both count the same records.  Dropping
-// only exact duplicates keeps the result exact (K3 still removes the rest).
-constexpr uint32_t kDedupSlots = 1u << 17;
-constexpr uint32_t kDedupWords = kDedupSlots / 32;
-
-template <bool kDedup>
-__device__ __forceinline__ void dedup_tile_begin(uint32_t* bm, uint32_t* s_epoch, uint32_t* s_flag,
-                                                 const uint64_t* __restrict__ kin, uint64_t tb) {
-    if (!kDedup) return;
-    if (threadIdx.x == 0) {
-        const uint32_t f = (uint32_t)kin[tb];
-        *s_flag = f != *s_epoch;
-        *s_epoch = f;
-    }
-    __syncthreads();
-    if (*s_flag) {
-        for (uint32_t i = threadIdx.x; i < kDedupWords; i += kBlock) bm[i] = 0;
-        __syncthreads();
-    }
-}
-
-template <bool kDedup>
-__device__ __forceinline__ bool dedup_keep(uint64_t raw, uint32_t epoch, uint32_t* bm) {
-    if (!kDedup) return true;
-    const uint64_t slot = raw >> 32;
-    if (slot >= kDedupSlots || (uint32_t)raw != epoch) return true;
-    const uint32_t bit = 1u << (slot & 31);
-    return !(atomicOr(&bm[slot >> 5], bit) & bit);
-}
-
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).  Same
 // tile grid and item mapping as the scatter.
-template <bool kDedup>
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
-                                                       int shift, uint32_t nchunks, uint64_t* __restrict__ table,
-                                                       const uint32_t* __restrict__ remap) {
+                                                       int shift, uint32_t dmask, uint32_t nchunks,
+                                                       uint64_t* __restrict__ table) {
     __shared__ uint32_t cnt[kWaves][kRadix];
-    __shared__ uint32_t bm[kDedup ? kDedupWords : 1];
-    __shared__ uint32_t s_epoch, s_flag;
     for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&cnt[0][0])[i] = 0;
-    if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint32_t* mine = cnt[wave_id()];
     const uint64_t tofs = (uint64_t)wave_id() * 64 * kSortItems + lane_id();
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
-        dedup_tile_begin<kDedup>(bm, &s_epoch, &s_flag, keys, tb);
-        const uint32_t epoch = s_epoch;
         uint64_t raw[kSortItems];
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
@@ -202,11 +144,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
             raw[k] = idx < hi ? keys[idx] : 0ull;
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
-            if (tb + tofs + (uint64_t)k * 64 < hi && dedup_keep<kDedup>(raw[k], epoch, bm))
-                atomicAdd(&mine[(uint32_t)(remap_key(raw[k], remap) >> shift) & (kRadix - 1)], 1u);
-        }
-        if (kDedup) __syncthreads();  // bitmap users done before the next tile may clear it
+        for (int k = 0; k < kSortItems; k++)
+            if (tb + tofs + (uint64_t)k * 64 < hi) atomicAdd(&mine[(uint32_t)(raw[k] >> shift) & dmask], 1u);
     }
     __syncthreads();
     for (int d = threadIdx.x; d < kRadix; d += kBlock) {
@@ -221,38 +160,38 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 // tile_base + w*64*kSortItems + k*64 + l, so (w, k, l) order == index order.
 // Ranks inside a wave come from a 64-lane match on the digit (8 ballots);
 // the tile is reordered by digit in LDS and written out in runs.
-template <bool kHasVals, bool kDedup>
+// kept (optional): workgroup b reads [b*chunk, b*chunk + kept[b]) — the
+// compacted ranges k_sort0_compact leaves — instead of [b*chunk, (b+1)*chunk).
+// dbits <= kRadixBits: digit width of this pass (fewer buckets -> longer runs
+// per tile -> better coalesced stores).
+template <bool kHasVals>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                           const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
-                                                          uint64_t n, uint64_t chunk, int shift, uint32_t nchunks,
-                                                          const uint64_t* __restrict__ table,
-                                                          const uint32_t* __restrict__ remap) {
+                                                          uint64_t n, uint64_t chunk, int shift, int dbits,
+                                                          uint32_t nchunks, const uint64_t* __restrict__ table,
+                                                          const uint64_t* __restrict__ kept) {
     __shared__ uint64_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[kHasVals ? kSortTile : 1];
     __shared__ uint32_t s_wcnt[kWaves][kRadix];
     __shared__ uint32_t s_tstart[kRadix];
     __shared__ uint64_t s_run[kRadix];
     __shared__ uint64_t s_scan[kWaves + 1];
-    __shared__ uint32_t bm[kDedup ? kDedupWords : 1];
-    __shared__ uint32_t s_epoch, s_flag;
     static_assert(kRadix == kBlock, "one digit per thread");
 
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const uint32_t dmask = (1u << dbits) - 1u;
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = kept ? lo + kept[blockIdx.x] : (lo + chunk < n ? lo + chunk : n);
     s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
-    if (t == 0) s_epoch = 0xFFFFFFFFu;
     const uint64_t lt = lanemask_lt();
 
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
 #pragma unroll
         for (int ww = 0; ww < kWaves; ww++) s_wcnt[ww][t] = 0;
         __syncthreads();
-        dedup_tile_begin<kDedup>(bm, &s_epoch, &s_flag, kin, tb);
-        const uint32_t epoch = s_epoch;
         uint64_t key[kSortItems];
         uint32_t val[kSortItems];
         uint32_t rank[kSortItems];
-        uint32_t keep = 0;
         const uint64_t wbase = tb + (uint64_t)w * 64 * kSortItems + l;
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
@@ -262,20 +201,16 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
         }
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
-            const bool ok = wbase + (uint64_t)k * 64 < hi && dedup_keep<kDedup>(key[k], epoch, bm);
-            keep |= (uint32_t)ok << k;
-            if (ok) key[k] = remap_key(key[k], remap);
-        }
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
-            const bool valid = (keep >> k) & 1u;
-            const uint32_t d = (uint32_t)(key[k] >> shift) & (kRadix - 1);
+            const bool valid = wbase + (uint64_t)k * 64 < hi;
+            const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
             uint64_t m = __ballot(valid);
 #pragma unroll
             for (int b = 0; b < kRadixBits; b++) {
-                const bool bit = (d >> b) & 1;
-                const uint64_t bb = __ballot(bit);
-                m &= bit ? bb : ~bb;
+                if (b < dbits) {
+                    const bool bit = (d >> b) & 1;
+                    const uint64_t bb = __ballot(bit);
+                    m &= bit ? bb : ~bb;
+                }
             }
             uint32_t r = 0;
             if (valid) {
@@ -299,8 +234,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
-            if ((keep >> k) & 1u) {
-                const uint32_t d = (uint32_t)(key[k] >> shift) & (kRadix - 1);
+            if (wbase + (uint64_t)k * 64 < hi) {
+                const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
                 const uint32_t pos = s_wcnt[w][d] + rank[k];
                 s_keys[pos] = key[k];
                 if (kHasVals) s_vals[pos] = val[k];
@@ -313,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
             const uint32_t p = j * kBlock + t;
             if (p < tile_n) {
                 const uint64_t k = s_keys[p];
-                const uint32_t d = (uint32_t)(k >> shift) & (kRadix - 1);
+                const uint32_t d = (uint32_t)(k >> shift) & dmask;
                 const uint64_t dst = s_run[d] + (p - s_tstart[d]);
                 kout[dst] = k;
                 if (kHasVals) vout[dst] = s_vals[p];
