@@ -253,6 +253,37 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     return II_OK;
 }
 
+// K3: distinct (lexid, id0) pairs of the sorted records r[0, n), their
+// posting byte offsets (P[U] = all posting bytes) and each word's first pair
+// (post_start[V] = U).  Sets c->U.
+static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n) {
+    CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
+    CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
+    CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
+    uint64_t* uniq = P_<uint64_t>(c->uniq);
+    uint64_t* Pp = P_<uint64_t>(c->P);
+    uint64_t* ps = P_<uint64_t>(c->pstart);
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    if (n == 0) {
+        HIPCK(hipMemsetAsync(ps + c->V, 0, sizeof(uint64_t), c->st));
+        HIPCK(hipMemsetAsync(Pp, 0, sizeof(uint64_t), c->st));
+        c->U = 0;
+        return II_OK;
+    }
+    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kUniqTile - 1) / kUniqTile);
+    const uint64_t chunk = ((n + nch - 1) / nch + kUniqTile - 1) / kUniqTile * kUniqTile;
+    nch = (n + chunk - 1) / chunk;
+    uint64_t* part = P_<uint64_t>(c->partial);
+    k_uniq_reduce<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part);
+    k_scan_partials<<<1, kBlock, 0, c->st>>>(part, (uint32_t)nch, ps + c->V);
+    k_scan_partials<<<1, kBlock, 0, c->st>>>(part + kMaxChunks, (uint32_t)nch, totals + 6);
+    k_uniq_apply<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part, uniq, Pp, ps);
+    HIPCK(hipGetLastError());
+    CK(read_u64(c, ps + c->V, &c->U));
+    HIPCK(hipMemcpyAsync(Pp + c->U, totals + 6, sizeof(uint64_t), hipMemcpyDeviceToDevice, c->st));
+    return II_OK;
+}
+
 // ----------------------------------------------------------------- lifecycle
 extern "C" int ii_open(ii_ctx** out, int device) {
     if (!out) return II_ERR_ARG;
@@ -272,7 +303,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_c0) HIPCK(hipEventCreate(&e));
-    if (grow(c->partial, sizeof(uint64_t) * (kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
+    if (grow(c->partial, sizeof(uint64_t) * (2 * kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
         return II_ERR_NOMEM;
@@ -659,13 +690,8 @@ static int local_reduce(ii_ctx* c) {
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
 
-    // ---- K3: unique (word, file) pairs and posting starts
-    CK(grow(c->uniq, sizeof(uint64_t) * Tk));
-    CK(grow(c->pstart, sizeof(uint64_t) * (V + 1)));
-    uint64_t* uniq = P_<uint64_t>(c->uniq);
-    uint64_t* ps = P_<uint64_t>(c->pstart);
-    CK(run_scan(c, OpUnique{r, uniq, ps}, Tk, ps + V));
-    CK(read_u64(c, ps + V, &c->U));
+    // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
+    CK(run_unique(c, r, Tk));
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;
     c->have_pairs = true;
@@ -704,12 +730,10 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     HIPCK(hipEventRecord(c->ev[5], c->st));
 
     // ---- K5: format "word:[ids]\n" lines
-    CK(grow(c->P, sizeof(uint64_t) * (c->U + 1)));
     CK(grow(c->loff, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->letter_off, sizeof(uint64_t) * (II_ALPHABET + 1)));
     uint64_t* Pp = P_<uint64_t>(c->P);
     uint64_t* loff = P_<uint64_t>(c->loff);
-    CK(run_scan(c, OpPostBytes{uniq, Pp}, c->U, Pp + c->U));
     CK(run_scan(c, OpLineOff{ov, P_<uint32_t>(c->llen), ps, Pp, loff}, V, totals + 2));
     CK(read_u64(c, totals + 2, &c->out_bytes));
     CK(grow(c->out, std::max<uint64_t>(c->out_bytes, 16)));
@@ -885,11 +909,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
-    CK(grow(c->uniq, sizeof(uint64_t) * NP));
-    CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
-    uint64_t* ps = P_<uint64_t>(c->pstart);
-    CK(run_scan(c, OpUnique{r, P_<uint64_t>(c->uniq), ps}, NP, ps + c->V));
-    CK(read_u64(c, ps + c->V, &c->U));
+    CK(run_unique(c, r, NP));
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)(p1 + p2);
     c->have_pairs = true;

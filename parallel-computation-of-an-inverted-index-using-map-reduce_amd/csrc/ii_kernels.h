@@ -454,22 +454,39 @@ __device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, co
 // with 16-B loads; the byte before a window comes from the neighbour lane, or
 // a 1-byte load for lane 0 of a wave; the rare start whose keep decision lies
 // past its window walks the text in HBM (kept_starts with nothing staged).
+// kept tokens among the starts of the 16-B window v at text position g
+__device__ __forceinline__ uint32_t window_kept(const uint4& v, uint64_t g, const uint8_t* __restrict__ text,
+                                                uint64_t nbytes) {
+    const Classes cl = classify16(v);
+    uint32_t prev = (uint32_t)__shfl_up((int)v.w, 1, 64) >> 24;
+    if ((threadIdx.x & 63) == 0) prev = (g > 0 && g - 1 < nbytes) ? text[g - 1] : 32u;
+    const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
+    return __popc(kept_starts(starts, cl, nullptr, text, nbytes, g, 0, 0));
+}
+
 __global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                       uint64_t* __restrict__ chunk_cnt) {
     __shared__ uint64_t s_scan[kWaves + 1];
     constexpr int kWinsPerLane = (int)(kChunk / 16 / kBlock);
+    constexpr int kInFlight = 8;
     const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
     const int t = threadIdx.x;
     uint64_t kept = 0;
-#pragma unroll 4
-    for (int j = 0; j < kWinsPerLane; j++) {
-        const uint64_t g = chunk_lo + 16 * ((uint64_t)kBlock * j + t);
-        const uint4 v = load16(text, nbytes, (int64_t)g);
-        const Classes cl = classify16(v);
-        uint32_t prev = (uint32_t)__shfl_up((int)v.w, 1, 64) >> 24;
-        if ((t & 63) == 0) prev = (g > 0 && g - 1 < nbytes) ? text[g - 1] : 32u;
-        const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
-        kept += __popc(kept_starts(starts, cl, nullptr, text, nbytes, g, 0, 0));
+    if (chunk_lo + kChunk + 16 <= nbytes) {  // interior chunk: plain 16-B loads, 8 in flight per lane
+        for (int jb = 0; jb < kWinsPerLane; jb += kInFlight) {
+            uint4 v[kInFlight];
+#pragma unroll
+            for (int u = 0; u < kInFlight; u++)
+                v[u] = *reinterpret_cast<const uint4*>(text + chunk_lo + 16 * ((uint64_t)kBlock * (jb + u) + t));
+#pragma unroll
+            for (int u = 0; u < kInFlight; u++)
+                kept += window_kept(v[u], chunk_lo + 16 * ((uint64_t)kBlock * (jb + u) + t), text, nbytes);
+        }
+    } else {
+        for (int j = 0; j < kWinsPerLane; j++) {
+            const uint64_t g = chunk_lo + 16 * ((uint64_t)kBlock * j + t);
+            kept += window_kept(load16(text, nbytes, (int64_t)g), g, text, nbytes);
+        }
     }
     uint64_t tot;
     (void)block_excl_scan(kept, &tot, s_scan);
@@ -898,15 +915,43 @@ __device__ __forceinline__ uint32_t next_letter(const uint8_t* __restrict__ text
     return 26u;
 }
 
+// byte mask (0xFF per selected byte) of the low 4 bits of m, one bit per byte
+__device__ __forceinline__ uint32_t byte_mask4(uint32_t m) { return ((m & 0xFu) * 0x00204081u & 0x01010101u) * 0xFFu; }
+
+// Two tokens whose raw bytes agree up to their first whitespace / NUL, letters
+// compared case-insensitively, clean to the same word (main.c:105-111).
+// Returns 1 = same word, 0 = undecided (the letter walk decides).
+__device__ __forceinline__ int same_raw_token(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t a, uint64_t b) {
+    for (uint32_t off = 0; off < 4 * (uint32_t)kMaxWord; off += 16) {
+        const uint4 A = global_block16(text, nbytes, a + off), B = global_block16(text, nbytes, b + off);
+        const Classes ca = classify16(A), cb = classify16(B);
+        const uint32_t ta = ca.ws | ca.nul, tb = cb.ws | cb.nul;
+        const uint32_t ea = ta ? __builtin_ctz(ta) : 16u, eb = tb ? __builtin_ctz(tb) : 16u;
+        if (ea != eb) return 0;
+        const uint32_t live = ea == 16u ? 0xFFFFu : (1u << ea) - 1u;
+        if ((ca.letter ^ cb.letter) & live) return 0;
+        const uint32_t wa[4] = {A.x, A.y, A.z, A.w}, wb[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t lowa = wa[k] | (byte_mask4(ca.letter >> (4 * k)) & 0x20202020u);
+            const uint32_t lowb = wb[k] | (byte_mask4(cb.letter >> (4 * k)) & 0x20202020u);
+            if ((lowa ^ lowb) & byte_mask4(live >> (4 * k))) return 0;
+        }
+        if (ea < 16u) return 1;
+    }
+    return 0;
+}
+
 // Exactness check for hashed keys: every long token must spell the same word
-// as its slot's representative occurrence.
+// as its slot's representative occurrence.  Most occurrences repeat the
+// representative's bytes (same_raw_token); the rest are walked letter by letter.
 __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         const LongTok* __restrict__ longs, uint64_t nlong,
                                                         const uint64_t* __restrict__ rep, uint64_t* counters) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nlong; i += (uint64_t)gridDim.x * kBlock) {
         LongTok lt = longs[i];
         uint64_t a = lt.pos, b = rep[lt.slot];
-        if (a == b) continue;
+        if (a == b || same_raw_token(text, nbytes, a, b)) continue;
         uint32_t na = 0, nb = 0;
         for (;;) {
             uint32_t la = next_letter(text, nbytes, &a, &na);
@@ -1190,21 +1235,102 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
     }
 }
 
-// ---------------------------------------------------------------- K3 unique
-// Records sorted by (lexid, fid): keep the first of each equal run (distinct
-// fileIDs per word, main.c:176-184); post_start[lexid] = first unique index.
-struct OpUnique {
-    const uint64_t* rec;
-    uint64_t* uniq;
-    uint64_t* post_start;
-    __device__ uint64_t value(uint64_t i) const { return i == 0 || rec[i] != rec[i - 1]; }
-    __device__ void emit(uint64_t i, uint64_t ex, uint64_t v) const {
-        if (!v) return;
-        uint64_t r = rec[i];
-        uniq[ex] = r;
-        if (i == 0 || (r >> 32) != (rec[i - 1] >> 32)) post_start[r >> 32] = ex;
+// ---------------------------------------------------------------- K3 unique + posting bytes
+// Records sorted by (lexid, id0): the first of each equal run is a distinct
+// (word, file) pair (main.c:176-184, add_number main.c:67-77); its posting
+// "id0+1" takes its digits + 1 bytes (the following ' ' or ']',
+// main.c:228-234).  One reduce-then-scan yields both prefixes: uniq[u] = the
+// pair, P[u] = byte offset of its posting (P[p] - P[post_start[w]] is the
+// offset inside word w's list) and post_start[lexid] = the word's first pair.
+constexpr int kUniqItems = 4;                        // consecutive records per thread
+constexpr int kUniqTile = kUniqItems * kBlock;
+
+// digits of v = id0 + 1 <= 2^32 (1..10), branch-free
+__device__ __forceinline__ uint32_t id_digits(uint64_t v) {
+    return 1u + (v >= 10ull) + (v >= 100ull) + (v >= 1000ull) + (v >= 10000ull) + (v >= 100000ull) +
+           (v >= 1000000ull) + (v >= 10000000ull) + (v >= 100000000ull) + (v >= 1000000000ull);
+}
+
+// thread's kUniqItems records at i0: distinct-pair count and posting bytes
+__device__ __forceinline__ void uniq_items(const uint64_t* __restrict__ rec, uint64_t i0, uint64_t hi, uint64_t (&r)[kUniqItems],
+                                           uint32_t& first, uint64_t& cnt, uint64_t& bytes) {
+    uint64_t prev = (i0 > 0 && i0 <= hi) ? rec[i0 - 1] : ~0ull;
+    first = 0;
+    cnt = bytes = 0;
+#pragma unroll
+    for (int q = 0; q < kUniqItems; q++) {
+        const uint64_t i = i0 + q;
+        r[q] = i < hi ? rec[i] : 0ull;
+        if (i < hi && (i == 0 || r[q] != prev)) {
+            first |= 1u << q;
+            cnt++;
+            bytes += id_digits((r[q] & 0xFFFFFFFFull) + 1) + 1;
+        }
+        prev = r[q];
     }
-};
+}
+
+// part[b] = distinct pairs of workgroup b's range, part[kMaxChunks + b] = their posting bytes
+__global__ __launch_bounds__(kBlock) void k_uniq_reduce(const uint64_t* __restrict__ rec, uint64_t n, uint64_t chunk,
+                                                        uint64_t* __restrict__ part) {
+    __shared__ uint64_t lds[2][kWaves];
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint64_t ac = 0, ab = 0;
+    for (uint64_t base = lo; base < hi; base += kUniqTile) {
+        uint64_t r[kUniqItems], c, b;
+        uint32_t first;
+        uniq_items(rec, base + (uint64_t)kUniqItems * threadIdx.x, hi, r, first, c, b);
+        ac += c;
+        ab += b;
+    }
+    ac = wave_sum(ac);
+    ab = wave_sum(ab);
+    if (lane_id() == 0) {
+        lds[0][wave_id()] = ac;
+        lds[1][wave_id()] = ab;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tc = 0, tb = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) {
+            tc += lds[0][w];
+            tb += lds[1][w];
+        }
+        part[blockIdx.x] = tc;
+        part[kMaxChunks + blockIdx.x] = tb;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restrict__ rec, uint64_t n, uint64_t chunk,
+                                                       const uint64_t* __restrict__ part, uint64_t* __restrict__ uniq,
+                                                       uint64_t* __restrict__ P, uint64_t* __restrict__ post_start) {
+    __shared__ uint64_t lds[2 * kWaves];
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint64_t run_c = part[blockIdx.x], run_b = part[kMaxChunks + blockIdx.x];
+    for (uint64_t base = lo; base < hi; base += kUniqTile) {
+        const uint64_t i0 = base + (uint64_t)kUniqItems * threadIdx.x;
+        uint64_t r[kUniqItems], c, b, ec, eb, tc, tb;
+        uint32_t first;
+        uniq_items(rec, i0, hi, r, first, c, b);
+        block_excl_scan2(c, b, ec, eb, tc, tb, lds);
+        uint64_t u = run_c + ec, o = run_b + eb;
+        uint64_t prev = (i0 > 0 && i0 <= hi) ? rec[i0 - 1] : ~0ull;
+#pragma unroll
+        for (int q = 0; q < kUniqItems; q++) {
+            if ((first >> q) & 1u) {
+                uniq[u] = r[q];
+                P[u] = o;
+                if (i0 + q == 0 || (r[q] >> 32) != (prev >> 32)) post_start[r[q] >> 32] = u;
+                u++;
+                o += id_digits((r[q] & 0xFFFFFFFFull) + 1) + 1;
+            }
+            prev = r[q];
+        }
+        run_c += tc;
+        run_b += tb;
+    }
+}
 
 // ---------------------------------------------------------------- K4 order
 // key = letter << dbits | (dmax - df): ascending == (letter, df desc); the
@@ -1222,12 +1348,6 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restric
 }
 
 // ---------------------------------------------------------------- K5 format
-__device__ __forceinline__ uint32_t ndigits(uint64_t v) {
-    uint32_t d = 1;
-    while (v >= 10) { v /= 10; d++; }
-    return d;
-}
-
 __device__ __forceinline__ void write_word(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t key, uint64_t rep,
                                            uint32_t len, uint8_t* __restrict__ o) {
     if ((key & 0xFull) == 0) {
@@ -1240,14 +1360,6 @@ __device__ __forceinline__ void write_word(const uint8_t* __restrict__ text, uin
         }
     }
 }
-
-// bytes of one posting: digits of id0+1 plus the following ' ' or ']'
-struct OpPostBytes {
-    const uint64_t* uniq;
-    uint64_t* P;
-    __device__ uint64_t value(uint64_t i) const { return ndigits((uniq[i] & 0xFFFFFFFFull) + 1) + 1; }
-    __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { P[i] = ex; }
-};
 
 // line bytes in final order: "word:[" + postings + "\n"
 struct OpLineOff {
@@ -1285,11 +1397,23 @@ __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict
     for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < U; p += (uint64_t)gridDim.x * kBlock) {
         uint64_t r = uniq[p];
         uint32_t w = (uint32_t)(r >> 32);
-        uint64_t id = (r & 0xFFFFFFFFull) + 1;
-        uint64_t ps = post_start[w];
-        uint64_t o = loff[w] + lex_len[w] + 2 + (P[p] - P[ps]);
-        uint32_t nd = ndigits(id);
-        for (int i = (int)nd - 1; i >= 0; i--) { out[o + i] = (uint8_t)('0' + id % 10); id /= 10; }
+        const uint64_t id = (r & 0xFFFFFFFFull) + 1;
+        const uint64_t ps = post_start[w];
+        const uint64_t o = loff[w] + lex_len[w] + 2 + (P[p] - P[ps]);
+        const uint32_t nd = id_digits(id);
+        if (id <= 0xFFFFFFFFull) {
+            uint32_t v = (uint32_t)id;
+            for (int i = (int)nd - 1; i >= 0; i--) {
+                out[o + i] = (uint8_t)('0' + v % 10u);
+                v /= 10u;
+            }
+        } else {
+            uint64_t v = id;
+            for (int i = (int)nd - 1; i >= 0; i--) {
+                out[o + i] = (uint8_t)('0' + v % 10u);
+                v /= 10u;
+            }
+        }
         out[o + nd] = (p + 1 == post_start[w + 1]) ? ']' : ' ';
     }
 }

@@ -54,6 +54,32 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total,
     return wbase + inc - v;
 }
 
+// Exclusive block scan of two values at once (one pair of barriers).
+__device__ __forceinline__ void block_excl_scan2(uint64_t a, uint64_t b, uint64_t& ea, uint64_t& eb, uint64_t& ta,
+                                                 uint64_t& tb, uint64_t* lds /*2*kWaves*/) {
+    const uint64_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+    if (lane_id() == 63) {
+        lds[wave_id()] = ia;
+        lds[kWaves + wave_id()] = ib;
+    }
+    __syncthreads();
+    uint64_t wa = 0, wb = 0;
+    ta = tb = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        const uint64_t sa = lds[w], sb = lds[kWaves + w];
+        if (w < wave_id()) {
+            wa += sa;
+            wb += sb;
+        }
+        ta += sa;
+        tb += sb;
+    }
+    __syncthreads();
+    ea = wa + ia - a;
+    eb = wb + ib - b;
+}
+
 // ----------------------------------------------------------------------------
 // Device-wide exclusive scan over n items.  Op provides
 //   uint64_t value(uint64_t i)                 (the item)
