@@ -169,12 +169,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scatter_ms, emit_ms = [], []
+    scatter_ms, emit_ms, phase_ms = [], [], []
     for _ in range(a.steps):
         step()
         st = idx.stats()
         scatter_ms.append(st.scatter_ms_avg)
         emit_ms.append(st.emit_ms)
+        phase_ms.append(st.ms_sort + st.ms_reduce)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -194,6 +195,15 @@ def main():
         em_ms = sum(emit_ms) / len(emit_ms)
         em_achieved = st.emit_bytes / (em_ms * 1e-3) / 1e9 if em_ms > 0 else 0.0
         traffic = pmc_traffic()
+        # sort + segmented-reduce phase (K2 token sort + K3 unique), SURVEY §8d byte model:
+        # first pass 8 B per record read + 8 B per kept record written; each scatter pass
+        # 16 B per kept record; each later histogram pass 8 B per kept record; the unique
+        # scan reads the kept records twice and writes 16 B (pair + posting offset) per pair
+        T, Tk, U = st.tokens, st.sorted_records, st.pairs
+        sp = max(1, st.sort_passes)
+        ph_bytes = 8 * T + 8 * Tk + sp * 16 * Tk + (sp - 1) * 8 * Tk + 2 * 8 * Tk + 16 * U
+        ph_ms = sum(phase_ms) / len(phase_ms)
+        ph_achieved = ph_bytes / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(text, off, a.cpu_sample_bytes)
         line = {
             "metric": "indexed input GB/s (whole node) + % of HBM peak BW",
@@ -221,6 +231,14 @@ def main():
                               "achieved": round(sc_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(sc_achieved / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
+            "roofline_sort_phase": {"bound": "hbm", "phase": "token sort + segmented unique (K2 + K3)",
+                                    "achieved": round(ph_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(ph_achieved / HBM_PEAK_GBS, 4), "bytes_per_step": ph_bytes,
+                                    "ms_per_step": round(ph_ms, 4),
+                                    "first_pass": {"kernel": "k_sort0_compact", "ms": round(st.sort0_ms, 4),
+                                                   "bytes": st.sort0_bytes,
+                                                   "achieved": round(st.sort0_bytes / (st.sort0_ms * 1e-3) / 1e9, 1)
+                                                   if st.sort0_ms > 0 else 0.0}},
             "cpu_baseline": cpu,
             "phases_ms": {k: round(getattr(st, k), 3) for k in
                           ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total",

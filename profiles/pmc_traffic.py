@@ -9,8 +9,8 @@ alone, then WRITE_SIZE alone: they cannot share a pass on gfx950), each under
 `timeout -s KILL`.  `summarize` averages the counters per dispatch of every
 kernel and applies the gfx950 correction: FETCH_SIZE counts half the bytes of
 a wide (16 B/lane) streaming read, so the read side is calibrated on
-k_tok_count, whose read bytes are known exactly (the text, B bytes + the
-512-byte halo per 64 KiB chunk); WRITE_SIZE is taken as reported.
+k_tok_count, whose read bytes are known (the text, B bytes, read once with
+16-B loads); WRITE_SIZE is taken as reported.
 """
 import csv
 import collections
@@ -19,10 +19,11 @@ import os
 import subprocess
 import sys
 
-KERNELS = "k_tok_emit|k_tok_count|k_radix_scatter|k_radix_hist"
+KERNELS = "k_tok_emit|k_tok_count|k_tok_resolve|k_sort0_compact|k_radix_scatter|k_radix_hist|k_uniq"
 
 
 def run(out, bench_args):
+    os.makedirs(out, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
         d = os.path.join(out, ctr.lower())
@@ -60,8 +61,7 @@ def summarize(out):
     B = meta.get("config", {}).get("bytes_per_rank")
     factor = None
     if B and "ii::k_tok_count" in res and "FETCH_SIZE" in res["ii::k_tok_count"]:
-        chunks = (B + 65535) // 65536
-        known = B + 512 * chunks
+        known = B
         factor = known / (res["ii::k_tok_count"]["FETCH_SIZE"] * 1024)
     for name, v in res.items():
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
