@@ -519,7 +519,13 @@ constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 // "word id" lines, main.c:116).  First letters are counted per chunk
 // (chunk_hist = the partial_<letter>.txt line counts); tokens of > 12 letters
 // are queued for the hash-collision check.
-constexpr int kWin = 4;                          // 16-B windows per lane per round
+#ifndef II_K1_WIN
+#define II_K1_WIN 4
+#endif
+#ifndef II_K1_MINWAVES
+#define II_K1_MINWAVES 4
+#endif
+constexpr int kWin = II_K1_WIN;                  // 16-B windows per lane per round
 constexpr int kRound = kWin * 16 * kBlock;       // 16 KiB of text per round
 constexpr int kRoundWins = kRound / 16;          // windows per round
 constexpr int kRoundStaged = kRound + kHalo;     // bytes staged in LDS after the left piece
@@ -617,32 +623,36 @@ __device__ __forceinline__ uint32_t spread4(uint32_t x) {
     return (x | (x << 1)) & 0x55u;
 }
 
-// Cooperative hot-bucket probe: every lane holds one token (key, home, fast);
-// the wave probes its 64 tokens' buckets in 4 rounds of 16, 4 lanes per
-// bucket each loading one 16-B quarter, so a bucket costs one cache line
-// access per instruction (a lane-private 64-B probe would cost four).  The
-// owner lane gets its bucket's 8-bit match / occupied masks.
-__device__ __forceinline__ void wave_bucket_probe(const Table& t, uint64_t key, uint32_t home, uint64_t fastmask,
-                                                  uint32_t& match, uint32_t& full) {
+// Cooperative hot-bucket probe: every lane holds one token (key, home); the
+// wave probes its 64 tokens' buckets in 4 rounds of 16, 4 lanes per bucket
+// each loading one 16-B quarter, so a bucket costs one cache line access per
+// instruction (a lane-private 64-B probe would cost four).  probe_issue starts
+// the loads (unconditionally: a lane without a key probes the bucket of key 0,
+// harmlessly); probe_finish gives the owner lane its bucket's 8-bit match /
+// occupied masks.  Split so that a later token batch's loads can be in flight
+// while an earlier batch resolves.
+struct ProbeParts {
+    ulonglong2 q[4];
+};
+__device__ __forceinline__ void probe_issue(const Table& t, uint32_t home, ProbeParts& pp) {
     const int l = lane_id();
-    const uint32_t quarter = 2u * (l & 3);
-    ulonglong2 part[4];
+    const unsigned long long* base = t.keys + 2u * (l & 3);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int src = 16 * r + (l >> 2);
-        const uint32_t h = (uint32_t)__shfl((int)home, src, 64);
-        part[r] = make_ulonglong2(0ull, 0ull);
-        if ((fastmask >> src) & 1ull)
-            part[r] = *reinterpret_cast<const ulonglong2*>(t.keys + (h & ~(uint32_t)(kBucket - 1)) + quarter);
+        const uint32_t h = (uint32_t)__shfl((int)home, 16 * r + (l >> 2), 64);
+        pp.q[r] = *reinterpret_cast<const ulonglong2*>(base + (h & ~(uint32_t)(kBucket - 1)));
     }
+}
+__device__ __forceinline__ void probe_finish(uint64_t key, const ProbeParts& pp, uint32_t& match, uint32_t& full) {
+    const int l = lane_id();
     match = full = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int src = 16 * r + (l >> 2);
         const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), src, 64) << 32) |
                            (uint32_t)__shfl((int)(uint32_t)key, src, 64);
-        const uint64_t m0 = __ballot(part[r].x == k), m1 = __ballot(part[r].y == k);
-        const uint64_t f0 = __ballot(part[r].x != 0ull), f1 = __ballot(part[r].y != 0ull);
+        const uint64_t m0 = __ballot(pp.q[r].x == k), m1 = __ballot(pp.q[r].y == k);
+        const uint64_t f0 = __ballot(pp.q[r].x != 0ull), f1 = __ballot(pp.q[r].y != 0ull);
         if ((l >> 4) == r) {
             const int b = 4 * (l & 15);
             match = spread4((uint32_t)(m0 >> b) & 0xFu) | (spread4((uint32_t)(m1 >> b) & 0xFu) << 1);
@@ -650,6 +660,66 @@ __device__ __forceinline__ void wave_bucket_probe(const Table& t, uint64_t key, 
         }
     }
 }
+
+// Two-lane form (II_K1_PROBE == 2): 32 tokens per round, 2 rounds; a lane
+// pair loads the two 16-B slot pairs that begin the key's probe order
+// (home's pair and the next one), so a probe reads 32 B.  known = the slots
+// seen.  A frequent word sits at or next to its home slot (it was inserted
+// while its bucket was still empty), so the short window decides almost
+// every token; the rest go to K1c.
+__device__ __forceinline__ void probe_issue2(const Table& t, uint32_t home, ProbeParts& pp) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t h = (uint32_t)__shfl((int)home, 32 * r + (l >> 1), 64);
+        const uint32_t pair = (((h & (kBucket - 1)) >> 1) + (l & 1)) & 3u;
+        pp.q[r] = *reinterpret_cast<const ulonglong2*>(t.keys + (h & ~(uint32_t)(kBucket - 1)) + 2u * pair);
+    }
+}
+__device__ __forceinline__ void probe_finish2(uint64_t key, uint32_t home, const ProbeParts& pp, uint32_t& match,
+                                              uint32_t& full, uint32_t& known) {
+    const int l = lane_id();
+    const uint32_t p0 = (home & (kBucket - 1)) >> 1, p1 = (p0 + 1) & 3u;
+    match = full = 0;
+    known = (3u << (2 * p0)) | (3u << (2 * p1));
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int src = 32 * r + (l >> 1);
+        const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), src, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)key, src, 64);
+        const uint64_t m0 = __ballot(pp.q[r].x == k), m1 = __ballot(pp.q[r].y == k);
+        const uint64_t f0 = __ballot(pp.q[r].x != 0ull), f1 = __ballot(pp.q[r].y != 0ull);
+        if ((l >> 5) == r) {
+            const int b = 2 * (l & 31);
+            const uint32_t a0 = (uint32_t)(m0 >> b) & 3u, a1 = (uint32_t)(m1 >> b) & 3u;
+            const uint32_t c0 = (uint32_t)(f0 >> b) & 3u, c1 = (uint32_t)(f1 >> b) & 3u;
+            match = ((a0 & 1u) << (2 * p0)) | ((a1 & 1u) << (2 * p0 + 1)) | ((a0 >> 1) << (2 * p1)) |
+                    ((a1 >> 1) << (2 * p1 + 1));
+            full = ((c0 & 1u) << (2 * p0)) | ((c1 & 1u) << (2 * p0 + 1)) | ((c0 >> 1) << (2 * p1)) |
+                   ((c1 >> 1) << (2 * p1 + 1));
+        }
+    }
+}
+__device__ __forceinline__ uint32_t rotr8(uint32_t x, uint32_t s) { return ((x >> s) | (x << (8 - s))) & 0xFFu; }
+// bucket_resolve for a partly seen bucket: a match is the slot; otherwise the
+// first empty slot inside the seen prefix of the probe order is claimed; a
+// seen prefix with no empty slot leaves the word to K1c.
+__device__ __forceinline__ uint32_t bucket_resolve2(const Table& t, uint32_t match, uint32_t full, uint32_t known,
+                                                    uint64_t key, uint32_t home, uint64_t pos) {
+    const uint32_t h7 = home & (kBucket - 1);
+    const uint32_t bbase = home - h7;
+    if (match) return bbase + __builtin_ctz(match);
+    const uint32_t kr = rotr8(known, h7);
+    const uint32_t prefix = kr & ~(kr + 1u);  // probe positions 0.. seen without a gap
+    const uint32_t er = rotr8(~full & 0xFFu, h7) & prefix;
+    if (!er) return kSlotNone;
+    const uint32_t p = (h7 + __builtin_ctz(er)) & (kBucket - 1);
+    return table_claim(t, bbase + p, key, pos) == key ? bbase + p : kSlotNone;
+}
+
+#ifndef II_K1_PROBE
+#define II_K1_PROBE 2
+#endif
 
 // Unresolved token of a chunk (K1b -> K1c), one u32: chunk-relative start
 // (16 bits) | chunk-relative token index << 16 (15 bits) | general path << 31.
@@ -700,7 +770,7 @@ __device__ __forceinline__ void lane_hist_flush(const uint32_t (&lc)[7], uint32_
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram.
 template <int kAblate = 0>
-__global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
+__global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                      const uint64_t* __restrict__ file_start,
                                                      const uint32_t* __restrict__ file_id, uint32_t nfiles,
                                                      const uint64_t* __restrict__ chunk_off, Table tab,
@@ -768,33 +838,62 @@ __global__ __launch_bounds__(kBlock) void k_tok_emit(const uint8_t* __restrict__
         const bool fsame = s_f[0] == s_f[1];
         const uint32_t fid0 = s_f[2];
         const uint32_t qbase = (uint32_t)(out - cbase), pbase = (uint32_t)(lo - chunk_lo);
-        // 3. keys + cooperative hot-bucket probes, one token per lane; no barrier
-        for (uint32_t b0 = 0; b0 < ntok; b0 += kBlock) {
+        // 3. keys + cooperative hot-bucket probes, one token per lane, no
+        //    barrier (two batches in flight per wave cost a wave per SIMD of
+        //    occupancy and measured slower)
+        struct Tok {
+            uint64_t key;
+            uint32_t p, home, first;
+            bool valid, fast;
+        };
+        auto tok_key = [&](Tok& k, uint32_t b0) {
             const uint32_t q = b0 + t;
-            const bool valid = q < ntok;
-            const uint32_t p = valid ? s_off[q] : 0u;
-            TokKey k{0ull, 0u, 0u};
-            const bool fast = valid && round_fast_key(s_text, s_mask, p, k);
-            const uint32_t home = hot_slot(k.key, tab.seed);
-            if (!(kAblate & 4)) lane_hist_add(lc, k.first, fast);
+            k.valid = q < ntok;
+            k.p = k.valid ? s_off[q] : 0u;
+            TokKey tk{0ull, 0u, 0u};
+            k.fast = k.valid && round_fast_key(s_text, s_mask, k.p, tk);
+            k.key = tk.key;
+            k.first = tk.first;
+            k.home = hot_slot(tk.key, tab.seed);
+            if (!(kAblate & 4)) lane_hist_add(lc, tk.first, k.fast);
+        };
+        auto tok_finish = [&](const Tok& k, const ProbeParts& pp, uint32_t b0) {
+            const uint32_t q = b0 + t;
             uint32_t slot = kSlotNone;
             if (kAblate & 1) {
-                if (fast) slot = home;
+                if (k.fast) slot = k.home;
             } else {
                 uint32_t match, full;
-                wave_bucket_probe(tab, k.key, home, __ballot(fast), match, full);
-                if (fast) slot = bucket_resolve(tab, match, full, k.key, home, lo + p);
+#if II_K1_PROBE == 2
+                uint32_t known;
+                probe_finish2(k.key, k.home, pp, match, full, known);
+                if (k.fast) slot = bucket_resolve2(tab, match, full, known, k.key, k.home, lo + k.p);
+#else
+                probe_finish(k.key, pp, match, full);
+                if (k.fast) slot = bucket_resolve(tab, match, full, k.key, k.home, lo + k.p);
+#endif
             }
-            const bool resolved = fast && slot != kSlotNone;
+            const bool resolved = k.fast && slot != kSlotNone;
             if (resolved) {
-                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, s_f[0], s_f[1], lo + p)];
+                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, s_f[0], s_f[1], lo + k.p)];
                 rec[out + q] = ((uint64_t)slot << 32) | f;
-            } else if (fast) {
+            } else if (k.fast) {
                 rec[out + q] = k.key;
             }
-            const bool pending = valid && !resolved;
+            const bool pending = k.valid && !resolved;
             const uint32_t pi = wave_append(&s_npend, pending);
-            if (pending) pend[cbase + pi] = (pbase + p) | ((qbase + q) << 16) | (fast ? 0u : kPendSlow);
+            if (pending) pend[cbase + pi] = (pbase + k.p) | ((qbase + q) << 16) | (k.fast ? 0u : kPendSlow);
+        };
+        for (uint32_t b0 = 0; b0 < ntok; b0 += kBlock) {
+            Tok k;
+            ProbeParts pp;
+            tok_key(k, b0);
+#if II_K1_PROBE == 2
+            if (!(kAblate & 1)) probe_issue2(tab, k.home, pp);
+#else
+            if (!(kAblate & 1)) probe_issue(tab, k.home, pp);
+#endif
+            tok_finish(k, pp, b0);
         }
         out += ntok;
     }
