@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--cpu-sample-bytes", type=float, default=48e6)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--gen-threads", type=int, default=16)
+    p.add_argument("--letter-split", choices=["balanced", "reference"], default="balanced",
+                   help="letter ownership of the N>1 exchange: histogram-balanced (SURVEY §8 f4) or the "
+                        "reference's 26/N reducer split (main.c:129-130)")
     return p.parse_args()
 
 
@@ -135,8 +138,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one process per GPU over RCCL (backend "nccl"); II_DIST_BACKEND=gloo rehearses the N>1 path on
+        # fewer GPUs (ranks share devices, collectives go through host memory) — never for measurements
+        backend = os.environ.get("II_DIST_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
 
@@ -159,7 +169,7 @@ def main():
     def step():
         idx.map_device(d_text.data_ptr(), nbytes, file_start, ids)
         if world > 1:  # local reduce -> letter-range all-to-allv (RCCL) -> owner merge + format
-            ii_dist.exchange_and_reduce(idx, id_bound)
+            ii_dist.exchange_and_reduce(idx, id_bound, balanced=a.letter_split == "balanced")
         else:
             idx.reduce(copy_text=False)
 
@@ -182,7 +192,7 @@ def main():
     dt = time.perf_counter() - t0
     st = idx.stats()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt / a.steps * 1e3
@@ -218,9 +228,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic Zipf corpus (tools/iigen.c, s~1, seed %d+1000*rank), device-resident" % a.seed,
-            "config": {"workload": "zipf %.0f GB x %d files/rank, vocab %d (BASELINE configs[2])" % (
+            "config": {"workload": "zipf %.3g GB x %d files/rank, vocab %d (BASELINE configs[2])" % (
                 nbytes / 1e9, a.files, a.vocab), "bytes_per_rank": nbytes, "files_per_rank": a.files,
-                "vocab": a.vocab, "parallelism": "shard-per-gpu x%d" % world},
+                "vocab": a.vocab, "parallelism": "shard-per-gpu x%d" % world,
+                "letter_split": a.letter_split if world > 1 else None},
             # dominant kernel: the tokenizer (K1b); algorithmic bytes = B + 8*T per launch
             "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
                          "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

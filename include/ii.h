@@ -157,6 +157,21 @@ int ii_reduce_local(ii_ctx *ctx);
  * id_bound = 1 + the largest id0 of all files of all GPUs.
  */
 int ii_export_plan(ii_ctx *ctx, int nparts, uint64_t *seg_bytes);
+
+/* Histogram-balanced letter ownership.  The reference's
+ * 26/G split (main.c:129-130) gives owners 4 % to 24 % of the work at G = 8;
+ * instead, part r may own the contiguous letters [letter_lo[r], letter_hi[r])
+ * chosen from a per-letter load:
+ *   ii_letter_load       -> distinct (word, file) pairs per first letter of
+ *                           this context's partial index (sum it over GPUs)
+ *   ii_balanced_letters  -> contiguous ranges minimising the largest part's
+ *                           load (pure host arithmetic; parts may be empty)
+ *   ii_export_plan_ranges-> ii_export_plan with those ranges (every GPU must
+ *                           pass the same ranges) */
+#define II_MAX_PARTS 64
+int ii_letter_load(ii_ctx *ctx, uint64_t pairs[II_ALPHABET]);
+int ii_balanced_letters(const uint64_t weight[II_ALPHABET], int nparts, int *letter_lo, int *letter_hi);
+int ii_export_plan_ranges(ii_ctx *ctx, int nparts, const int *letter_lo, const int *letter_hi, uint64_t *seg_bytes);
 int ii_export(ii_ctx *ctx, int nparts, void *d_send, const uint64_t *send_off);
 int ii_import(ii_ctx *ctx, int nparts, const void *d_recv, const uint64_t *recv_off, uint32_t id_bound);
 

@@ -96,6 +96,10 @@ def lib():
         L.ii_export_plan.argtypes = [ctypes.c_void_p, ctypes.c_int, u64p]
         L.ii_export.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, u64p]
         L.ii_import.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, u64p, ctypes.c_uint32]
+        i32p = ctypes.POINTER(ctypes.c_int)
+        L.ii_letter_load.argtypes = [ctypes.c_void_p, u64p]
+        L.ii_balanced_letters.argtypes = [u64p, ctypes.c_int, i32p, i32p]
+        L.ii_export_plan_ranges.argtypes = [ctypes.c_void_p, ctypes.c_int, i32p, i32p, u64p]
         _lib = L
     return _lib
 
@@ -172,6 +176,18 @@ class Index:
         _check(lib().ii_export_plan(self.h, nparts, out), "ii_export_plan")
         return list(out)
 
+    def export_plan_ranges(self, letter_lo, letter_hi):
+        n = len(letter_lo)
+        out = (ctypes.c_uint64 * n)()
+        _check(lib().ii_export_plan_ranges(self.h, n, (ctypes.c_int * n)(*letter_lo), (ctypes.c_int * n)(*letter_hi),
+                                           out), "ii_export_plan_ranges")
+        return list(out)
+
+    def letter_load(self):
+        out = (ctypes.c_uint64 * ALPHABET)()
+        _check(lib().ii_letter_load(self.h, out), "ii_letter_load")
+        return list(out)
+
     def export(self, nparts, d_send_ptr, send_off):
         _check(lib().ii_export(self.h, nparts, ctypes.c_void_p(d_send_ptr), _u64(send_off)), "ii_export")
 
@@ -203,6 +219,14 @@ def reducer_letters(r, R):
     lo, hi = ctypes.c_int(), ctypes.c_int()
     _check(lib().ii_reducer_letters(r, R, ctypes.byref(lo), ctypes.byref(hi)), "ii_reducer_letters")
     return lo.value, hi.value
+
+
+def balanced_letters(weights, parts):
+    """-> (letter_lo, letter_hi) lists, ii_balanced_letters."""
+    lo = (ctypes.c_int * parts)()
+    hi = (ctypes.c_int * parts)()
+    _check(lib().ii_balanced_letters(_u64(list(weights)), parts, lo, hi), "ii_balanced_letters")
+    return list(lo), list(hi)
 
 
 def partition(sizes, M):

@@ -22,11 +22,20 @@ def prefix(sizes):
     return off, acc
 
 
+def _host_staged(group):
+    """gloo moves host tensors only: device buffers are staged through host
+    memory (CPU tests and N>1 rehearsals on fewer GPUs, never measurements)."""
+    return dist.get_backend(group) == "gloo"
+
+
 def alltoallv_bytes(send, send_sizes, group=None):
     """Exchange variable-size byte segments: send[off_r : off_r + send_sizes[r]]
     goes to rank r.  Returns (recv, recv_sizes) with the segments from ranks
     0..world-1 back to back.  One count exchange + one all_to_all_single."""
     world = dist.get_world_size(group)
+    out_dev = send.device
+    if _host_staged(group) and send.is_cuda:
+        send = send.cpu()
     dev = send.device
     cnt = torch.tensor(send_sizes, dtype=torch.int64, device=dev)
     rcnt = torch.empty(world, dtype=torch.int64, device=dev)
@@ -35,15 +44,34 @@ def alltoallv_bytes(send, send_sizes, group=None):
     recv = torch.empty(sum(recv_sizes), dtype=torch.uint8, device=dev)
     dist.all_to_all_single(recv, send, output_split_sizes=recv_sizes, input_split_sizes=list(send_sizes),
                            group=group)
-    return recv, recv_sizes
+    return recv.to(out_dev), recv_sizes
 
 
-def exchange_and_reduce(idx, id_bound, group=None, copy_text=False):
+def owner_ranges(idx_loads, world):
+    """Histogram-balanced letter ranges from the per-letter
+    pair counts summed over all shards."""
+    import ii_ctypes
+    total = [sum(col) for col in zip(*idx_loads)]
+    return ii_ctypes.balanced_letters(total, world)
+
+
+def exchange_and_reduce(idx, id_bound, group=None, copy_text=False, balanced=False):
     """Local reduce -> export -> all-to-allv -> import -> order + format.
-    After it, idx holds the final text of this rank's letters
-    (ii_reducer_letters(rank, world)); the other letters are empty."""
+    After it, idx holds the final text of this rank's letters — the
+    reference's reducer map ii_reducer_letters(rank, world) (main.c:129-130),
+    or with balanced=True the histogram-balanced ranges every rank derives from
+    the same all-reduced letter loads; the other letters are empty.  Returns
+    (recv_sizes, (letter_lo, letter_hi))."""
+    import ii_ctypes
     world = dist.get_world_size(group)
-    sizes = idx.export_plan(world)
+    if balanced:
+        load = torch.tensor(idx.letter_load(), dtype=torch.int64, device="cpu" if _host_staged(group) else "cuda")
+        dist.all_reduce(load, group=group)
+        lo, hi = ii_ctypes.balanced_letters([int(x) for x in load.tolist()], world)
+    else:
+        lo, hi = zip(*[ii_ctypes.reducer_letters(r, world) for r in range(world)])
+        lo, hi = list(lo), list(hi)
+    sizes = idx.export_plan_ranges(lo, hi)
     send_off, total = prefix(sizes)
     send = torch.empty(max(total, 8), dtype=torch.uint8, device="cuda")
     idx.export(world, send.data_ptr(), send_off)
@@ -53,17 +81,24 @@ def exchange_and_reduce(idx, id_bound, group=None, copy_text=False):
         recv = torch.empty(8, dtype=torch.uint8, device="cuda")
     idx.import_(world, recv.data_ptr(), recv_off, id_bound)
     idx.reduce(copy_text=copy_text)
-    return recv_sizes
+    return recv_sizes, (lo, hi)
 
 
-def logical_shards_reduce(idxs, id_bound, copy_text=True):
+def logical_shards_reduce(idxs, id_bound, copy_text=True, balanced=False):
     """The same exchange among G contexts on ONE device (no collective): the
     "G logical shards on 1 device" mode of SURVEY.md §4 that exercises the
-    export/import logic when fewer GPUs are present."""
+    export/import logic when fewer GPUs are present.  Returns the owners'
+    (letter_lo, letter_hi)."""
+    import ii_ctypes
     G = len(idxs)
+    if balanced:
+        lo, hi = owner_ranges([ix.letter_load() for ix in idxs], G)
+    else:
+        lo, hi = zip(*[ii_ctypes.reducer_letters(r, G) for r in range(G)])
+        lo, hi = list(lo), list(hi)
     sends = []
     for ix in idxs:
-        sizes = ix.export_plan(G)
+        sizes = ix.export_plan_ranges(lo, hi)
         off, total = prefix(sizes)
         buf = torch.empty(max(total, 8), dtype=torch.uint8, device="cuda")
         ix.export(G, buf.data_ptr(), off)
@@ -75,3 +110,4 @@ def logical_shards_reduce(idxs, id_bound, copy_text=True):
         torch.cuda.synchronize()
         ix.import_(G, recv.data_ptr(), prefix(recv_sizes)[0], id_bound)
         ix.reduce(copy_text=copy_text)
+    return lo, hi

@@ -56,6 +56,7 @@ struct ii_ctx {
     DBuf woff, pts;
     uint64_t h_pts[3 * (II_ALPHABET + 1)] = {0};
     int planned_parts = 0;
+    int part_lo[II_MAX_PARTS] = {0}, part_hi[II_MAX_PARTS] = {0};  // letter range of every export part
 
     uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
     uint32_t retries = 0;
@@ -798,20 +799,52 @@ static inline uint64_t seg_bytes(uint64_t nw, uint64_t np, uint64_t arena) {
     return 64 + 8 * np + ((arena + 7) & ~7ull);
 }
 
-extern "C" int ii_export_plan(ii_ctx* c, int nparts, uint64_t* bytes_out) {
-    if (!c || nparts < 1 || !bytes_out) return II_ERR_ARG;
+static int plan_core(ii_ctx* c, int nparts, const int* lo_in, const int* hi_in, uint64_t* bytes_out) {
+    if (!c || nparts < 1 || nparts > II_MAX_PARTS || !bytes_out) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
+    for (int r = 0; r < nparts; r++) {
+        int lo, hi;
+        if (lo_in) {
+            lo = lo_in[r];
+            hi = hi_in[r];
+            // contiguous, in order, covering [0, 26)
+            if (lo < 0 || hi < lo || hi > II_ALPHABET || lo != (r ? c->part_hi[r - 1] : 0)) return II_ERR_ARG;
+        } else {
+            ii_reducer_letters(r, nparts, &lo, &hi);
+        }
+        c->part_lo[r] = lo;
+        c->part_hi[r] = hi;
+    }
+    if (c->part_hi[nparts - 1] != II_ALPHABET) return II_ERR_ARG;
     HIPCK(hipSetDevice(c->dev));
     if (!c->have_pairs) CK(local_reduce(c));
     CK(letter_points(c));
     for (int r = 0; r < nparts; r++) {
-        int lo, hi;
-        ii_reducer_letters(r, nparts, &lo, &hi);
-        const uint64_t* a = c->h_pts + 3 * lo;
-        const uint64_t* b = c->h_pts + 3 * hi;
+        const uint64_t* a = c->h_pts + 3 * c->part_lo[r];
+        const uint64_t* b = c->h_pts + 3 * c->part_hi[r];
         bytes_out[r] = seg_bytes(b[0] - a[0], b[1] - a[1], b[2] - a[2]);
     }
     c->planned_parts = nparts;
+    return II_OK;
+}
+
+extern "C" int ii_export_plan(ii_ctx* c, int nparts, uint64_t* bytes_out) {
+    return plan_core(c, nparts, nullptr, nullptr, bytes_out);
+}
+
+extern "C" int ii_export_plan_ranges(ii_ctx* c, int nparts, const int* letter_lo, const int* letter_hi,
+                                     uint64_t* bytes_out) {
+    if (!letter_lo || !letter_hi) return II_ERR_ARG;
+    return plan_core(c, nparts, letter_lo, letter_hi, bytes_out);
+}
+
+extern "C" int ii_letter_load(ii_ctx* c, uint64_t pairs[II_ALPHABET]) {
+    if (!c || !pairs) return II_ERR_ARG;
+    if (!c->mapped) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    if (!c->have_pairs) CK(local_reduce(c));
+    CK(letter_points(c));
+    for (int l = 0; l < II_ALPHABET; l++) pairs[l] = c->h_pts[3 * (l + 1) + 1] - c->h_pts[3 * l + 1];
     return II_OK;
 }
 
@@ -821,8 +854,7 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
     HIPCK(hipSetDevice(c->dev));
     for (int r = 0; r < nparts; r++) {
         if (send_off[r] & 7) return II_ERR_ARG;
-        int lo, hi;
-        ii_reducer_letters(r, nparts, &lo, &hi);
+        const int lo = c->part_lo[r], hi = c->part_hi[r];
         const uint64_t* a = c->h_pts + 3 * lo;
         const uint64_t* b = c->h_pts + 3 * hi;
         const uint64_t nw = b[0] - a[0], np = b[1] - a[1], ab = b[2] - a[2];
@@ -996,6 +1028,39 @@ extern "C" int ii_reducer_letters(int r, int R, int* lo, int* hi) {
     if (R < 1 || r < 0 || r >= R || !lo || !hi) return II_ERR_ARG;
     *lo = (II_ALPHABET / R) * r;                                       // main.c:129
     *hi = (r == R - 1) ? II_ALPHABET : (II_ALPHABET / R) * (r + 1);    // main.c:130
+    return II_OK;
+}
+
+// Contiguous letter ranges for nparts owners minimising the largest summed
+// weight (linear partition: DP for the optimum, then a greedy fill to it, so
+// earlier parts take as much as the optimum allows).  Pure host arithmetic.
+extern "C" int ii_balanced_letters(const uint64_t* w, int nparts, int* lo, int* hi) {
+    if (!w || nparts < 1 || nparts > II_MAX_PARTS || !lo || !hi) return II_ERR_ARG;
+    const int L = II_ALPHABET;
+    uint64_t pre[II_ALPHABET + 1] = {0};
+    for (int l = 0; l < L; l++) pre[l + 1] = pre[l] + w[l];
+    // best[k][i]: the smallest possible largest part when letters [0, i) go to k parts
+    std::vector<std::vector<uint64_t>> best(nparts + 1, std::vector<uint64_t>(L + 1, UINT64_MAX));
+    best[0][0] = 0;
+    for (int k = 1; k <= nparts; k++)
+        for (int i = 0; i <= L; i++)
+            for (int j = 0; j <= i; j++)
+                if (best[k - 1][j] != UINT64_MAX)
+                    best[k][i] = std::min(best[k][i], std::max(best[k - 1][j], pre[i] - pre[j]));
+    const uint64_t opt = best[nparts][L];
+    int r = 0;
+    uint64_t sum = 0;
+    lo[0] = 0;
+    for (int l = 0; l < L; l++) {
+        if (sum + w[l] > opt && r < nparts - 1) {
+            hi[r] = l;
+            lo[++r] = l;
+            sum = 0;
+        }
+        sum += w[l];
+    }
+    hi[r] = L;
+    for (int k = r + 1; k < nparts; k++) lo[k] = hi[k] = L;
     return II_OK;
 }
 

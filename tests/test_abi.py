@@ -103,3 +103,37 @@ def test_open_without_gpu_reports_nodev():
     with pytest.raises(ii_ctypes.IIError) as e:
         ii_ctypes.Index(0)
     assert e.value.code == -8
+
+
+def _brute_best(w, parts):
+    """Smallest possible largest part of a contiguous split of w into parts."""
+    import functools
+
+    @functools.lru_cache(None)
+    def f(i, k):
+        if i == len(w):
+            return 0
+        if k == 1:
+            return sum(w[i:])
+        return min(max(sum(w[i:j]), f(j, k - 1)) for j in range(i, len(w) + 1))
+    return f(0, parts)
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 5, 8])
+def test_balanced_letters_optimal_and_contiguous(parts):
+    import random
+    rng = random.Random(parts)
+    for trial in range(12):
+        w = [rng.choice([0, 0, 1, 5, 100, rng.randint(0, 10 ** 6)]) for _ in range(26)]
+        lo, hi = ii_ctypes.balanced_letters(w, parts)
+        assert lo[0] == 0 and hi[-1] == 26
+        for r in range(parts):
+            assert lo[r] <= hi[r]
+            if r:
+                assert lo[r] == hi[r - 1]
+        largest = max(sum(w[lo[r]:hi[r]]) for r in range(parts))
+        if parts <= 3:
+            assert largest == _brute_best(tuple(w), parts)
+        # never worse than the reference's 26/parts split (main.c:129-130)
+        ref = max(sum(w[a:b]) for a, b in (ii_ctypes.reducer_letters(r, parts) for r in range(parts)))
+        assert largest <= ref

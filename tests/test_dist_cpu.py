@@ -71,3 +71,38 @@ def test_alltoallv_bytes_gloo(world):
 
 def test_prefix():
     assert ii_dist.prefix([3, 0, 5]) == ([0, 3, 3], 8)
+
+
+def _balanced_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ii_ctypes
+        g = torch.Generator().manual_seed(7 + rank)
+        load = torch.randint(0, 10 ** 6, (26,), generator=g, dtype=torch.int64)
+        total = load.clone()
+        dist.all_reduce(total)
+        q.put((rank, ii_ctypes.balanced_letters([int(x) for x in total.tolist()], world),
+               [int(x) for x in total.tolist()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_balanced_owner_ranges_agree_gloo():
+    # every rank derives the same histogram-balanced owner ranges from the
+    # all-reduced letter loads (the N>1 exchange of bench.py --gpus N)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict((r, (rng, tot)) for r, rng, tot in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0] == out[1]
+    (lo, hi), tot = out[0]
+    assert lo[0] == 0 and hi[-1] == 26 and lo[1] == hi[0]

@@ -162,7 +162,7 @@ def test_zipf_medium_vs_oracle(idx):
 
 
 # ---------------------------------------------------------------- multi-GPU exchange logic
-def shard_and_merge(text, off, G, id_bound=None):
+def shard_and_merge(text, off, G, id_bound=None, balanced=False):
     """G logical shards on one device: files split by the reference's size
     heuristic (ii_partition), each shard mapped in its own context, letter
     ranges exchanged (ii_export / ii_import) and formatted by their owner."""
@@ -181,10 +181,12 @@ def shard_and_merge(text, off, G, id_bound=None):
         ix = ii_ctypes.Index(0)
         ix.map_host(bytes(t), o, fids)
         idxs.append(ix)
-    ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else n)
+    los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else n, balanced=balanced)
     merged = {}
     for g, ix in enumerate(idxs):
-        lo, hi = ii_ctypes.reducer_letters(g, G)
+        lo, hi = los[g], his[g]
+        if not balanced:
+            assert (lo, hi) == ii_ctypes.reducer_letters(g, G)
         got = ix.letters()
         for l in range(26):
             ch = chr(97 + l)
@@ -208,3 +210,10 @@ def test_logical_shards_zipf_vs_oracle():
     off = off.tolist()
     text = t.tobytes()
     assert_same(shard_and_merge(text, off, 4), oracle_index(text, off, list(range(300))), "zipf G=4")
+
+
+@pytest.mark.parametrize("case,G", [("config2", 3), ("zipf_small", 8), ("edge", 4)])
+def test_logical_shards_balanced_letters(case, G):
+    # histogram-balanced owners: same output, other ownership
+    text, off, ids, expected = case_arrays(case)
+    assert_same(shard_and_merge(text, off, G, balanced=True), expected, "%s G=%d balanced" % (case, G))
