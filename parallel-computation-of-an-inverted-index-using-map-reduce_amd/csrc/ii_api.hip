@@ -191,12 +191,12 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     if (n <= 1 || hi <= lo) return II_OK;
     if (remap0 && v) return II_ERR_INTERNAL;
     uint64_t nch = 0, chunk = 0;
-    auto regrid = [&](uint64_t m) {
-        nch = std::min<uint64_t>(kMaxChunks, (m + kSortTile - 1) / kSortTile);
-        chunk = ((m + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
+    auto regrid = [&](uint64_t m, uint64_t tile) {
+        nch = std::min<uint64_t>(kMaxChunks, (m + tile - 1) / tile);
+        chunk = ((m + nch - 1) / nch + tile - 1) / tile * tile;
         nch = (m + chunk - 1) / chunk;
     };
-    regrid(n);
+    regrid(n, remap0 ? (uint64_t)kCTile : (uint64_t)kSortTile);  // the first pass's chunks are whole compact tiles
     CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
     CK(grow(c->kept, sizeof(uint64_t) * kMaxChunks));
     uint64_t* table = P_<uint64_t>(c->rtable);
@@ -214,7 +214,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-            k_sort0_compact<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table, remap0,
+            k_sort0_compact<<<(uint32_t)nch, kCBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table, remap0,
                                                                  *k2, kept);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
@@ -244,7 +244,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n;
             if (n_out) *n_out = n;
             if (n <= 1) break;
-            regrid(n);
+            regrid(n, kSortTile);
         } else {
             std::swap(*k, *k2);
             if (kv) std::swap(*v, *v2);

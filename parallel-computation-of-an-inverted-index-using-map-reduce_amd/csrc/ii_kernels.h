@@ -1245,25 +1245,28 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // kept[b] = records kept by workgroup b; pass 0's scatter reads
 // [lo, lo + kept[b]) back.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+constexpr int kCBlock = 512;                    // 8 waves share one 64 KiB dedup bitmap
+constexpr int kCWaves = kCBlock / 64;
+constexpr int kCTile = kSortItems * kCBlock;    // records per tile (a multiple of kSortTile)
 
-__global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
-                                                          int shift, uint32_t dmask, uint32_t nchunks,
-                                                          uint64_t* __restrict__ table,
-                                                          const uint32_t* __restrict__ remap,
-                                                          uint64_t* __restrict__ kout, uint64_t* __restrict__ kept) {
-    __shared__ uint32_t cnt[kWaves][kRadix];
+__global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
+                                                           int shift, uint32_t dmask, uint32_t nchunks,
+                                                           uint64_t* __restrict__ table,
+                                                           const uint32_t* __restrict__ remap,
+                                                           uint64_t* __restrict__ kout, uint64_t* __restrict__ kept) {
+    __shared__ uint32_t cnt[kCWaves][kRadix];
     __shared__ uint32_t bm[kDedupWords];
-    __shared__ uint32_t s_wtot[kWaves];
+    __shared__ uint32_t s_wtot[kCWaves];
     __shared__ uint32_t s_epoch, s_flag;
     const int w = wave_id(), l = lane_id();
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kCWaves * kRadix; i += kCBlock) (&cnt[0][0])[i] = 0;
     if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     const uint64_t tofs = (uint64_t)w * 64 * kSortItems + l;
     const uint64_t lt = lanemask_lt();
     uint64_t o = lo;  // next output position
-    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
+    for (uint64_t tb = lo; tb < hi; tb += kCTile) {
         if (threadIdx.x == 0) {
             const uint32_t f = (uint32_t)keys[tb];
             s_flag = f != s_epoch;
@@ -1271,7 +1274,7 @@ __global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __rest
         }
         __syncthreads();
         if (s_flag) {
-            for (uint32_t i = threadIdx.x; i < kDedupWords; i += kBlock) bm[i] = 0;
+            for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
             __syncthreads();
         }
         const uint32_t epoch = s_epoch;
@@ -1279,7 +1282,7 @@ __global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __rest
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
-            raw[k] = idx < hi ? keys[idx] : 0ull;
+            raw[k] = idx < hi ? ld_nt(keys + idx) : 0ull;
         }
         uint32_t keep = 0, wcount = 0;
         uint32_t pos[kSortItems];
@@ -1296,11 +1299,15 @@ __global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __rest
             wcount += (uint32_t)__popcll(b);
             keep |= (uint32_t)ok << k;
         }
+        // the remap gathers of the kept records are in flight across the barrier
+        uint32_t lex[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) lex[k] = ((keep >> k) & 1u) ? remap[raw[k] >> 32] : 0u;
         if (l == 0) s_wtot[w] = wcount;
         __syncthreads();
         uint32_t wbase = 0, ttot = 0;
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ww++) {
+        for (int ww = 0; ww < kCWaves; ww++) {
             const uint32_t c = s_wtot[ww];
             if (ww < w) wbase += c;
             ttot += c;
@@ -1308,18 +1315,18 @@ __global__ __launch_bounds__(kBlock) void k_sort0_compact(const uint64_t* __rest
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
             if ((keep >> k) & 1u) {
-                const uint64_t r = ((uint64_t)remap[raw[k] >> 32] << 32) | (raw[k] & 0xFFFFFFFFull);
-                kout[o + wbase + pos[k]] = r;
+                const uint64_t r = ((uint64_t)lex[k] << 32) | (raw[k] & 0xFFFFFFFFull);
+                st_nt(kout + o + wbase + pos[k], r);
                 atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
             }
         }
         o += ttot;
         __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
     }
-    for (int d = threadIdx.x; d < kRadix; d += kBlock) {
+    for (int d = threadIdx.x; d < kRadix; d += kCBlock) {
         uint32_t tt = 0;
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ww++) tt += cnt[ww][d];
+        for (int ww = 0; ww < kCWaves; ww++) tt += cnt[ww][d];
         table[(uint64_t)d * nchunks + blockIdx.x] = tt;
     }
     if (threadIdx.x == 0) kept[blockIdx.x] = o - lo;
@@ -1341,8 +1348,9 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
 // main.c:228-234).  One reduce-then-scan yields both prefixes: uniq[u] = the
 // pair, P[u] = byte offset of its posting (P[p] - P[post_start[w]] is the
 // offset inside word w's list) and post_start[lexid] = the word's first pair.
-constexpr int kUniqItems = 4;                        // consecutive records per thread
-constexpr int kUniqTile = kUniqItems * kBlock;
+constexpr int kUniqItems = 4;                        // records per thread per tile
+constexpr int kUniqTile = kUniqItems * kBlock;       // item q of thread t: tile base + q * kBlock + t (coalesced)
+static_assert(kUniqItems * 16 <= 64, "per-item prefixes travel as 16-bit fields of one u64");
 
 // digits of v = id0 + 1 <= 2^32 (1..10), branch-free
 __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
@@ -1350,23 +1358,28 @@ __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
            (v >= 1000000ull) + (v >= 10000000ull) + (v >= 100000000ull) + (v >= 1000000000ull);
 }
 
-// thread's kUniqItems records at i0: distinct-pair count and posting bytes
-__device__ __forceinline__ void uniq_items(const uint64_t* __restrict__ rec, uint64_t i0, uint64_t hi, uint64_t (&r)[kUniqItems],
-                                           uint32_t& first, uint64_t& cnt, uint64_t& bytes) {
-    uint64_t prev = (i0 > 0 && i0 <= hi) ? rec[i0 - 1] : ~0ull;
-    first = 0;
+// The thread's records of the tile at base and, per item, whether it starts a
+// distinct pair (1 in the 16-bit field q of cnt) and its posting bytes (field
+// q of bytes).  The previous record comes from the neighbour lane.
+__device__ __forceinline__ void uniq_items(const uint64_t* __restrict__ rec, uint64_t base, uint64_t hi,
+                                           uint64_t (&r)[kUniqItems], uint64_t (&prev)[kUniqItems], uint64_t& cnt,
+                                           uint64_t& bytes) {
     cnt = bytes = 0;
 #pragma unroll
     for (int q = 0; q < kUniqItems; q++) {
-        const uint64_t i = i0 + q;
-        r[q] = i < hi ? rec[i] : 0ull;
-        if (i < hi && (i == 0 || r[q] != prev)) {
-            first |= 1u << q;
-            cnt++;
-            bytes += id_digits((r[q] & 0xFFFFFFFFull) + 1) + 1;
+        const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
+        r[q] = i < hi ? rec[i] : ~0ull;
+        uint64_t pv = (uint64_t)__shfl_up((long long)r[q], 1, 64);
+        if (lane_id() == 0) pv = (i > 0 && i <= hi) ? rec[i - 1] : ~0ull;
+        prev[q] = pv;
+        if (i < hi && (i == 0 || r[q] != pv)) {
+            cnt |= 1ull << (16 * q);
+            bytes += (uint64_t)(id_digits((r[q] & 0xFFFFFFFFull) + 1) + 1) << (16 * q);
         }
-        prev = r[q];
     }
+}
+__device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
+    return (x & 0xFFFFull) + ((x >> 16) & 0xFFFFull) + ((x >> 32) & 0xFFFFull) + (x >> 48);
 }
 
 // part[b] = distinct pairs of workgroup b's range, part[kMaxChunks + b] = their posting bytes
@@ -1376,11 +1389,10 @@ __global__ __launch_bounds__(kBlock) void k_uniq_reduce(const uint64_t* __restri
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint64_t ac = 0, ab = 0;
     for (uint64_t base = lo; base < hi; base += kUniqTile) {
-        uint64_t r[kUniqItems], c, b;
-        uint32_t first;
-        uniq_items(rec, base + (uint64_t)kUniqItems * threadIdx.x, hi, r, first, c, b);
-        ac += c;
-        ab += b;
+        uint64_t r[kUniqItems], pv[kUniqItems], c, b;
+        uniq_items(rec, base, hi, r, pv, c, b);
+        ac += field16_sum(c);
+        ab += field16_sum(b);
     }
     ac = wave_sum(ac);
     ab = wave_sum(ab);
@@ -1408,26 +1420,25 @@ __global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restric
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint64_t run_c = part[blockIdx.x], run_b = part[kMaxChunks + blockIdx.x];
     for (uint64_t base = lo; base < hi; base += kUniqTile) {
-        const uint64_t i0 = base + (uint64_t)kUniqItems * threadIdx.x;
-        uint64_t r[kUniqItems], c, b, ec, eb, tc, tb;
-        uint32_t first;
-        uniq_items(rec, i0, hi, r, first, c, b);
+        uint64_t r[kUniqItems], pv[kUniqItems], c, b, ec, eb, tc, tb;
+        uniq_items(rec, base, hi, r, pv, c, b);
+        // 16-bit fields: no carries (a field sums at most kBlock pairs of <= 11 bytes)
         block_excl_scan2(c, b, ec, eb, tc, tb, lds);
-        uint64_t u = run_c + ec, o = run_b + eb;
-        uint64_t prev = (i0 > 0 && i0 <= hi) ? rec[i0 - 1] : ~0ull;
+        uint64_t rc = run_c, rb = run_b;
 #pragma unroll
         for (int q = 0; q < kUniqItems; q++) {
-            if ((first >> q) & 1u) {
+            if ((c >> (16 * q)) & 1ull) {
+                const uint64_t u = rc + ((ec >> (16 * q)) & 0xFFFFull);
                 uniq[u] = r[q];
-                P[u] = o;
-                if (i0 + q == 0 || (r[q] >> 32) != (prev >> 32)) post_start[r[q] >> 32] = u;
-                u++;
-                o += id_digits((r[q] & 0xFFFFFFFFull) + 1) + 1;
+                P[u] = rb + ((eb >> (16 * q)) & 0xFFFFull);
+                const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
+                if (i == 0 || (r[q] >> 32) != (pv[q] >> 32)) post_start[r[q] >> 32] = u;
             }
-            prev = r[q];
+            rc += (tc >> (16 * q)) & 0xFFFFull;
+            rb += (tb >> (16 * q)) & 0xFFFFull;
         }
-        run_c += tc;
-        run_b += tb;
+        run_c = rc;
+        run_b = rb;
     }
 }
 

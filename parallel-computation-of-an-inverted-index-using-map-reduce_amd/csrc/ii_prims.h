@@ -16,6 +16,18 @@ constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxChunks = 2048;      // workgroups of a reduce-then-scan launch
 
+// Streaming accesses with the non-temporal hint, where measured to help: the
+// histogram reads and the first token-sort pass (records read once; the slot
+// -> lexid remap it gathers from should stay in the per-XCD L2s).  The scatter
+// and the tokenizer measured slower with it (writes lose L2 combining).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t ld_nt(const uint64_t* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(uint64_t* p, uint64_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ uint4 ld_nt16(const void* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -167,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
-            raw[k] = idx < hi ? keys[idx] : 0ull;
+            raw[k] = idx < hi ? ld_nt(keys + idx) : 0ull;
         }
 #pragma unroll
         for (int k = 0; k < kSortItems; k++)
