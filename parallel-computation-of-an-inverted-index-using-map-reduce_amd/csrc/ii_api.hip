@@ -78,6 +78,8 @@ struct ii_ctx {
     hipEvent_t ev_c0[2] = {};  // around k_sort0_compact
     uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
     uint64_t n_pending = 0; // tokens K1b left to K1c
+    uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
+    uint64_t nch_map = 0;   // K1b chunks of the last map
     ii_stats stats;
 };
 
@@ -188,17 +190,26 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
                     bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr) {
     if (passes) *passes = 0;
     if (n_out) *n_out = n;
-    if (n <= 1 || hi <= lo) return II_OK;
+    if (hi <= lo || (n <= 1 && !remap0)) return II_OK;
     if (remap0 && v) return II_ERR_INTERNAL;
+    // first pass over K1's records: one workgroup per `group` K1b chunks
+    const uint64_t nch_in = c->nch_map;
+    const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
+    if (remap0 && (nch_in == 0 || group > kCMaxGroup)) return II_ERR_NOMEM;
     uint64_t nch = 0, chunk = 0;
     auto regrid = [&](uint64_t m, uint64_t tile) {
         nch = std::min<uint64_t>(kMaxChunks, (m + tile - 1) / tile);
         chunk = ((m + nch - 1) / nch + tile - 1) / tile * tile;
         nch = (m + chunk - 1) / chunk;
     };
-    regrid(n, remap0 ? (uint64_t)kCTile : (uint64_t)kSortTile);  // the first pass's chunks are whole compact tiles
+    if (remap0) {
+        nch = (nch_in + group - 1) / group;
+        chunk = 0;
+    } else {
+        regrid(n, kSortTile);
+    }
     CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
-    CK(grow(c->kept, sizeof(uint64_t) * kMaxChunks));
+    CK(grow(c->kept, sizeof(uint64_t) * 2 * kMaxChunks));
     uint64_t* table = P_<uint64_t>(c->rtable);
     uint64_t* kept = P_<uint64_t>(c->kept);
     const bool kv = v != nullptr;
@@ -214,8 +225,9 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-            k_sort0_compact<<<(uint32_t)nch, kCBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table, remap0,
-                                                                 *k2, kept);
+            k_sort0_compact<<<(uint32_t)nch, kCBlock, 0, c->st>>>(*k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in,
+                                                                 (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
+                                                                 table, remap0, *k2, kept);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
         } else {
@@ -359,7 +371,25 @@ extern "C" const char* ii_strerror(int code) {
 }
 
 // ----------------------------------------------------------------- map (K1)
-static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
+// K1 record layout: the fixed-capacity one (no counting pass) unless
+// II_REC_LAYOUT=dense or its buffers (12 B per K1b token slot, 6 B per text
+// byte) would take more than 40% of the device memory left.
+static bool use_fixed_capacity(ii_ctx* c, uint64_t nch, bool dense) {
+    if (dense) return false;
+    const char* e = getenv("II_REC_LAYOUT");
+    if (e && !strcmp(e, "dense")) return false;
+    if (e && !strcmp(e, "fixed")) return true;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const double held = (double)c->rec.cap + (double)c->pend.cap;
+    return 12.0 * (double)nch * (double)kChunkCap <= 0.4 * ((double)fr + held);
+}
+
+// dense: records of token k at rec[k] (the import path indexes them so)
+static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = false) {
     c->mapped = c->have_pairs = c->reduced = false;
     c->planned_parts = 0;
     c->host_valid = false;
@@ -381,25 +411,37 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         return II_OK;
     }
     const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
-    CK(grow(c->chunk_cnt, sizeof(uint64_t) * nch));
+    c->nch_map = nch;
+    CK(grow(c->chunk_cnt, sizeof(uint64_t) * (nch + 1)));
     CK(grow(c->chunk_hist, sizeof(uint32_t) * 26 * nch));
     uint64_t* chunk_cnt = P_<uint64_t>(c->chunk_cnt);
     const uint64_t* fstart = P_<uint64_t>(c->fstart);
     const uint32_t* fid = P_<uint32_t>(c->fid);
 
     k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, counters);
-    k_tok_count<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, chunk_cnt);
-    CK(run_scan(c, OpInPlace{chunk_cnt}, nch, totals));
+    HIPCK(hipMemsetAsync(chunk_cnt + nch, 0, sizeof(uint64_t), c->st));  // voff[nch] = T after the scan
+    c->rec_cap = use_fixed_capacity(c, nch, dense) ? kChunkCap : 0;
     uint64_t hv[2];
-    CK(read_u64(c, totals, &hv[0]));
-    CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
-    if (hv[1] & 4) return II_ERR_LAYOUT;
-    c->T = hv[0];
-    CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
-    CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
-    CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
+    if (c->rec_cap) {
+        CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
+        if (hv[1] & 4) return II_ERR_LAYOUT;
+        CK(grow(c->rec, sizeof(uint64_t) * nch * kChunkCap));
+        CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
+        c->T = 0;
+    } else {
+        k_tok_count<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, chunk_cnt);
+        CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
+        CK(read_u64(c, totals, &hv[0]));
+        CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
+        if (hv[1] & 4) return II_ERR_LAYOUT;
+        c->T = hv[0];
+        CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+        CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+        CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
+    }
     CK(grow(c->pend_cnt, sizeof(uint32_t) * nch));
-    if (c->long_cap < std::max<uint64_t>(1 << 16, c->T / 64)) c->long_cap = std::max<uint64_t>(1 << 16, c->T / 64);
+    const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;  // the long queue grows on overflow
+    if (c->long_cap < std::max<uint64_t>(1 << 16, t_est / 64)) c->long_cap = std::max<uint64_t>(1 << 16, t_est / 64);
 
     for (int attempt = 0;; attempt++) {
         if (attempt > 12) return II_ERR_INTERNAL;
@@ -412,12 +454,13 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
-        k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt, tab,
+        k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
+                                                       c->rec_cap, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt));
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         k_tok_resolve<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
-                                                           P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
+                                                           c->rec_cap, P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
                                                            P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                            P_<LongTok>(c->longs), c->long_cap);
         HIPCK(hipEventRecord(c->ev_res[1], c->st));
@@ -452,6 +495,11 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET]) {
         c->V = cnt[C_INSERT];
         CK(read_u64(c, totals + 5, &c->n_pending));
         break;
+    }
+    if (c->rec_cap) {  // chunk token counts -> voff (exclusive scan, voff[nch] = T)
+        CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
+        CK(read_u64(c, totals, &c->T));
+        CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
     }
     k_hist_reduce<<<26, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
     HIPCK(hipGetLastError());
@@ -681,10 +729,6 @@ static int local_reduce(ii_ctx* c) {
     uint64_t* r = P_<uint64_t>(c->rec);
     uint64_t* r2 = P_<uint64_t>(c->rec2);
     const int lb = std::max(1, bitlen(V - 1));
-    if (T == 1) {  // nothing to sort: remap in place
-        k_remap<<<1, kBlock, 0, c->st>>>(r, T, P_<uint32_t>(c->remap));
-        HIPCK(hipGetLastError());
-    }
     uint64_t Tk = T;
     CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap), &Tk));
     c->rec_sorted = r;
@@ -909,7 +953,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     const uint64_t fs0 = 0;
     const uint32_t id0 = 0;
     CK(set_files(c, &fs0, &id0, A ? 1 : 0));
-    CK(map_core(c, nullptr));  // tokenises the words: word k -> rec[k] = slot << 32
+    CK(map_core(c, nullptr, true));  // tokenises the words: word k -> rec[k] = slot << 32
     if (c->T != W) return II_ERR_INTERNAL;
     c->id_bound = id_bound;
     if (W == 0) {

@@ -500,6 +500,16 @@ struct LongTok {
 };
 constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 
+// Record layout of K1b / K1c.  Dense (cap == 0): chunk b's records start at
+// chunk_off[b], the exclusive scan of k_tok_count's counts.  Fixed capacity
+// (cap == kChunkCap): chunk b owns rec[b * cap, (b + 1) * cap) and pend
+// likewise, no counting pass; K1b leaves the chunk's token count in
+// chunk_off[b] and the first sort pass gathers the used prefixes.
+constexpr uint64_t kChunkCap = kChunk / 2;  // a token start follows a whitespace byte
+__device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap) {
+    return cap ? (uint64_t)blockIdx.x * cap : chunk_off[blockIdx.x];
+}
+
 // ---------------------------------------------------------------- K1b emit
 // A workgroup walks its 64 KiB chunk in rounds of 16 KiB: 4 windows of 16 B
 // per lane, window w = 256 j + lane, so each load instruction reads 1 KiB
@@ -773,7 +783,7 @@ template <int kAblate = 0>
 __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                      const uint64_t* __restrict__ file_start,
                                                      const uint32_t* __restrict__ file_id, uint32_t nfiles,
-                                                     const uint64_t* __restrict__ chunk_off, Table tab,
+                                                     uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                      uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt) {
     __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kRoundStaged];
@@ -794,7 +804,7 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
         s_f[2] = file_id[s_f[0]];
         s_npend = 0;
     }
-    const uint64_t cbase = chunk_off[blockIdx.x];
+    const uint64_t cbase = chunk_base(chunk_off, cap);
     uint64_t out = cbase;
     uint32_t lc[7] = {0, 0, 0, 0, 0, 0, 0};
     RoundRegs nxt;
@@ -900,7 +910,10 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
     lane_hist_flush(lc, s_hist);
     __syncthreads();
     if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
-    if (t == 0) pend_cnt[blockIdx.x] = s_npend;
+    if (t == 0) {
+        pend_cnt[blockIdx.x] = s_npend;
+        if (cap) chunk_off[blockIdx.x] = out - cbase;  // fixed-capacity layout: the chunk's token count
+    }
 }
 
 // K1c: the tokens K1b left unresolved, one per thread across the chunk —
@@ -911,7 +924,7 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
 __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         const uint64_t* __restrict__ file_start,
                                                         const uint32_t* __restrict__ file_id, uint32_t nfiles,
-                                                        const uint64_t* __restrict__ chunk_off,
+                                                        const uint64_t* __restrict__ chunk_off, uint64_t cap,
                                                         const uint32_t* __restrict__ pend,
                                                         const uint32_t* __restrict__ pend_cnt, Table tab,
                                                         uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
@@ -934,7 +947,7 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
         s_lcount = 0;
     }
     __syncthreads();
-    const uint64_t cbase = chunk_off[blockIdx.x];
+    const uint64_t cbase = chunk_base(chunk_off, cap);
     const bool fsame = s_f[0] == s_f[1];
     for (uint32_t i = t; i < n; i += kBlock) {
         const uint32_t e = pend[cbase + i];
@@ -1242,33 +1255,57 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 //  * replaces the slot by the word's lexicographic id (remap);
 //  * writes the kept records, in order, to kout[lo ...) and counts their
 //    pass-0 digit (digit-major table, as k_radix_hist).
-// kept[b] = records kept by workgroup b; pass 0's scatter reads
-// [lo, lo + kept[b]) back.
+// Workgroup b takes the K1b chunks [b * group, (b + 1) * group): virtual
+// record indices voff[c0] .. voff[c1] (voff = exclusive scan of the chunk
+// token counts), stored at c * cap + (i - voff[c]) in the fixed-capacity
+// layout or at i in the dense one (cap == 0).  Its kept records go to
+// kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
+// voff[c0], the range pass 0's scatter reads back.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
 constexpr int kCBlock = 512;                    // 8 waves share one 64 KiB dedup bitmap
 constexpr int kCWaves = kCBlock / 64;
-constexpr int kCTile = kSortItems * kCBlock;    // records per tile (a multiple of kSortTile)
+constexpr int kCTile = kSortItems * kCBlock;    // records per tile
+constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
+// LDS: 8 KiB counts + 64 KiB bitmap + 4 KiB offsets, so two workgroups fit a CU
 
-__global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
-                                                           int shift, uint32_t dmask, uint32_t nchunks,
-                                                           uint64_t* __restrict__ table,
+__global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __restrict__ keys,
+                                                           const uint64_t* __restrict__ voff, uint32_t nch_in,
+                                                           uint32_t group, uint64_t cap, int shift, uint32_t dmask,
+                                                           uint32_t nchunks, uint64_t* __restrict__ table,
                                                            const uint32_t* __restrict__ remap,
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept) {
     __shared__ uint32_t cnt[kCWaves][kRadix];
     __shared__ uint32_t bm[kDedupWords];
+    __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
     __shared__ uint32_t s_wtot[kCWaves];
     __shared__ uint32_t s_epoch, s_flag;
     const int w = wave_id(), l = lane_id();
+    const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
     for (int i = threadIdx.x; i < kCWaves * kRadix; i += kCBlock) (&cnt[0][0])[i] = 0;
+    const uint64_t lo = voff[c0], hi = voff[c0 + ng];
+    for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
     if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
     __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     const uint64_t tofs = (uint64_t)w * 64 * kSortItems + l;
     const uint64_t lt = lanemask_lt();
+    uint32_t g = 0;                   // this lane's chunk cursor (its indices only grow)
+    uint32_t gnext = s_voff[1];       // first WG-relative index past chunk g
     uint64_t o = lo;  // next output position
     for (uint64_t tb = lo; tb < hi; tb += kCTile) {
-        if (threadIdx.x == 0) {
-            const uint32_t f = (uint32_t)keys[tb];
+        uint64_t raw[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint64_t idx = tb + tofs + (uint64_t)k * 64;
+            uint64_t src = idx;
+            if (cap && idx < hi) {
+                const uint32_t ri = (uint32_t)(idx - lo);
+                while (ri >= gnext) gnext = s_voff[++g + 1];
+                src = (uint64_t)(c0 + g) * cap + (ri - s_voff[g]);
+            }
+            raw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
+        }
+        if (threadIdx.x == 0) {  // thread 0's item 0 is the tile's first record
+            const uint32_t f = (uint32_t)raw[0];
             s_flag = f != s_epoch;
             s_epoch = f;
         }
@@ -1278,12 +1315,6 @@ __global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __res
             __syncthreads();
         }
         const uint32_t epoch = s_epoch;
-        uint64_t raw[kSortItems];
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
-            const uint64_t idx = tb + tofs + (uint64_t)k * 64;
-            raw[k] = idx < hi ? ld_nt(keys + idx) : 0ull;
-        }
         uint32_t keep = 0, wcount = 0;
         uint32_t pos[kSortItems];
 #pragma unroll
@@ -1329,7 +1360,10 @@ __global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __res
         for (int ww = 0; ww < kCWaves; ww++) tt += cnt[ww][d];
         table[(uint64_t)d * nchunks + blockIdx.x] = tt;
     }
-    if (threadIdx.x == 0) kept[blockIdx.x] = o - lo;
+    if (threadIdx.x == 0) {
+        kept[blockIdx.x] = o - lo;
+        kept[kMaxChunks + blockIdx.x] = lo;
+    }
 }
 
 // ---------------------------------------------------------------- K2 support

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 // tile_base + w*64*kSortItems + k*64 + l, so (w, k, l) order == index order.
 // Ranks inside a wave come from a 64-lane match on the digit (8 ballots);
 // the tile is reordered by digit in LDS and written out in runs.
-// kept (optional): workgroup b reads [b*chunk, b*chunk + kept[b]) — the
+// kept (optional): workgroup b reads [kept[kMaxChunks + b], + kept[b]) — the
 // compacted ranges k_sort0_compact leaves — instead of [b*chunk, (b+1)*chunk).
 // dbits <= kRadixBits: digit width of this pass (fewer buckets -> longer runs
 // per tile -> better coalesced stores).
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
 
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
     const uint32_t dmask = (1u << dbits) - 1u;
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t lo = kept ? kept[kMaxChunks + blockIdx.x] : (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = kept ? lo + kept[blockIdx.x] : (lo + chunk < n ? lo + chunk : n);
     s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
     const uint64_t lt = lanemask_lt();

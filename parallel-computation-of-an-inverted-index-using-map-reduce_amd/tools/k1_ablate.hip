@@ -57,9 +57,9 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
         CK(hipMemset(tab.keys, 0, nslots * 8));
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
-        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, tab, rec, chist, pend, pcnt);
+        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, tab, rec, chist, pend, pcnt);
         CK(hipEventRecord(b));
-        k_tok_resolve<<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, pend, pcnt, tab, rec, chist, longs, lcap);
+        k_tok_resolve<<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap);
         CK(hipEventRecord(c));
         CK(hipEventSynchronize(c));
         float ms, ms2; CK(hipEventElapsedTime(&ms, a, b)); CK(hipEventElapsedTime(&ms2, b, c));

@@ -161,6 +161,46 @@ def test_zipf_medium_vs_oracle(idx):
     assert_same(idx.letters(), oracle_index(t, off, ids), "zipf48M")
 
 
+def dense_sparse_corpus():
+    """Empty K1b chunks (whitespace only), chunks at the fixed capacity (one
+    letter per two bytes: kChunk / 2 tokens) and ordinary text across files."""
+    rng = random.Random(5)
+    parts = [b" " * 200_000, b"".join(rng.choice([b"a ", b"B\t", b"c\n"]) for _ in range(70_000)),
+             b"\n" * 150_000]
+    t2, off2, _ = rand_corpus(11, 30, 20_000)
+    text = bytearray()
+    off = [0]
+    for p in parts + [t2[off2[i]:off2[i + 1]] for i in range(30)] + [b"x " * 40_000]:
+        text += p
+        off.append(len(text))
+    return bytes(text), off, list(range(len(off) - 1))
+
+
+def test_record_layouts_vs_oracle():
+    """K1's dense (counted) and fixed-capacity record layouts give the same index."""
+    text, off, ids = dense_sparse_corpus()
+    exp = oracle_index(text, off, ids)
+    counts = {}
+    for layout in ["dense", "fixed"]:
+        os.environ["II_REC_LAYOUT"] = layout
+        try:
+            ix = ii_ctypes.Index(0)
+            for case in ["config2", "edge"]:
+                t, o, i, e = case_arrays(case)
+                ix.map_host(t, o, i)
+                ix.reduce()
+                assert_same(ix.letters(), e, layout + " " + case)
+            ix.map_host(text, off, ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, layout)
+            st = ix.stats()
+            counts[layout] = (st.tokens, st.pairs, st.words)
+            ix.close()
+        finally:
+            del os.environ["II_REC_LAYOUT"]
+    assert counts["dense"] == counts["fixed"]
+
+
 # ---------------------------------------------------------------- multi-GPU exchange logic
 def shard_and_merge(text, off, G, id_bound=None, balanced=False):
     """G logical shards on one device: files split by the reference's size
