@@ -505,9 +505,21 @@ constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 // (cap == kChunkCap): chunk b owns rec[b * cap, (b + 1) * cap) and pend
 // likewise, no counting pass; K1b leaves the chunk's token count in
 // chunk_off[b] and the first sort pass gathers the used prefixes.
+// Inside its slot, chunk b's records start at a per-chunk rotation and wrap:
+// slots are 256 KiB apart and a Zipf chunk fills ~30 % of its slot, so
+// unrotated prefixes would all sit at the same low offsets of every slot and
+// load only the HBM channels those offsets interleave to.
 constexpr uint64_t kChunkCap = kChunk / 2;  // a token start follows a whitespace byte
+static_assert((kChunkCap & (kChunkCap - 1)) == 0, "slot rotation wraps with a mask");
+__device__ __forceinline__ uint32_t chunk_rot(uint32_t b) {
+    return (uint32_t)(((b * 2654435761u) >> 22) << 5) & (uint32_t)(kChunkCap - 1);  // 256-B steps
+}
 __device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap) {
     return cap ? (uint64_t)blockIdx.x * cap : chunk_off[blockIdx.x];
+}
+// index of the chunk's j-th record (cbase from chunk_base, rot = chunk_rot(b))
+__device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint64_t cap, uint32_t rot, uint32_t j) {
+    return cap ? cbase + ((j + rot) & (uint32_t)(kChunkCap - 1)) : cbase + j;
 }
 
 // ---------------------------------------------------------------- K1b emit
@@ -805,7 +817,8 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
         s_npend = 0;
     }
     const uint64_t cbase = chunk_base(chunk_off, cap);
-    uint64_t out = cbase;
+    const uint32_t rot = chunk_rot(blockIdx.x);
+    uint32_t out = 0;  // records emitted so far
     uint32_t lc[7] = {0, 0, 0, 0, 0, 0, 0};
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
@@ -847,7 +860,7 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
         __syncthreads();
         const bool fsame = s_f[0] == s_f[1];
         const uint32_t fid0 = s_f[2];
-        const uint32_t qbase = (uint32_t)(out - cbase), pbase = (uint32_t)(lo - chunk_lo);
+        const uint32_t qbase = out, pbase = (uint32_t)(lo - chunk_lo);
         // 3. keys + cooperative hot-bucket probes, one token per lane, no
         //    barrier (two batches in flight per wave cost a wave per SIMD of
         //    occupancy and measured slower)
@@ -884,11 +897,12 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
 #endif
             }
             const bool resolved = k.fast && slot != kSlotNone;
+            const uint64_t ri = rec_slot(cbase, cap, rot, out + q);
             if (resolved) {
                 const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, s_f[0], s_f[1], lo + k.p)];
-                rec[out + q] = ((uint64_t)slot << 32) | f;
+                rec[ri] = ((uint64_t)slot << 32) | f;
             } else if (k.fast) {
-                rec[out + q] = k.key;
+                rec[ri] = k.key;
             }
             const bool pending = k.valid && !resolved;
             const uint32_t pi = wave_append(&s_npend, pending);
@@ -912,7 +926,7 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
     if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
     if (t == 0) {
         pend_cnt[blockIdx.x] = s_npend;
-        if (cap) chunk_off[blockIdx.x] = out - cbase;  // fixed-capacity layout: the chunk's token count
+        if (cap) chunk_off[blockIdx.x] = out;  // fixed-capacity layout: the chunk's token count
     }
 }
 
@@ -952,7 +966,7 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
     for (uint32_t i = t; i < n; i += kBlock) {
         const uint32_t e = pend[cbase + i];
         const uint64_t pos = chunk_lo + (e & 0xFFFFu);
-        const uint64_t r = cbase + ((e >> 16) & 0x7FFFu);
+        const uint64_t r = rec_slot(cbase, cap, chunk_rot(blockIdx.x), (e >> 16) & 0x7FFFu);
         uint64_t key;
         uint32_t nlet = 0;
         if (e & kPendSlow) {
@@ -1300,7 +1314,7 @@ __global__ __launch_bounds__(kCBlock) void k_sort0_compact(const uint64_t* __res
             if (cap && idx < hi) {
                 const uint32_t ri = (uint32_t)(idx - lo);
                 while (ri >= gnext) gnext = s_voff[++g + 1];
-                src = (uint64_t)(c0 + g) * cap + (ri - s_voff[g]);
+                src = (uint64_t)(c0 + g) * cap + ((ri - s_voff[g] + chunk_rot(c0 + g)) & (uint32_t)(kChunkCap - 1));
             }
             raw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
         }

@@ -223,20 +223,32 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
     s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
     const uint64_t lt = lanemask_lt();
 
+    // the next tile's keys are loaded while this tile is ranked and written
+    uint64_t nkey[kSortItems];
+    uint32_t nval[kSortItems];
+    auto load_tile = [&](uint64_t tb) {
+        const uint64_t wb = tb + (uint64_t)w * 64 * kSortItems + l;
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint64_t idx = wb + (uint64_t)k * 64;
+            nkey[k] = idx < hi ? kin[idx] : ~0ull;
+            if (kHasVals) nval[k] = idx < hi ? vin[idx] : 0u;
+        }
+    };
+    if (lo < hi) load_tile(lo);
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
 #pragma unroll
         for (int ww = 0; ww < kWaves; ww++) s_wcnt[ww][t] = 0;
-        __syncthreads();
         uint64_t key[kSortItems];
         uint32_t val[kSortItems];
         uint32_t rank[kSortItems];
         const uint64_t wbase = tb + (uint64_t)w * 64 * kSortItems + l;
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
-            const uint64_t idx = wbase + (uint64_t)k * 64;
-            key[k] = idx < hi ? kin[idx] : ~0ull;
-            if (kHasVals) val[k] = idx < hi ? vin[idx] : 0u;
+            key[k] = nkey[k];
+            if (kHasVals) val[k] = nval[k];
         }
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
             const bool valid = wbase + (uint64_t)k * 64 < hi;
@@ -280,6 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
             }
         }
         __syncthreads();
+        if (tb + kSortTile < hi) load_tile(tb + kSortTile);
         const uint32_t tile_n = (uint32_t)all;
 #pragma unroll
         for (int j = 0; j < kSortItems; j++) {
