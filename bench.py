@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--cpu-sample-bytes", type=float, default=48e6)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--gen-threads", type=int, default=16)
+    p.add_argument("--io-bytes", type=float, default=2e9,
+                   help="bytes of the corpus written to files for the ii_map_files reader leg (0 = skip)")
     p.add_argument("--letter-split", choices=["balanced", "reference"], default="balanced",
                    help="letter ownership of the N>1 exchange: histogram-balanced (SURVEY §8 f4) or the "
                         "reference's 26/N reducer split (main.c:129-130)")
@@ -123,6 +125,42 @@ def cpu_baseline(text, off, sample_bytes):
     return {"value": round(sb / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": sample.replace("M=%d mappers, R=26 reducers" % cores, "oracle restatement, 1 thread"),
             "seconds": round(dt, 3)}
+
+
+def io_leg(idx, text, off, io_bytes, threads=16):
+    """End-to-end file leg, reported beside `value`, never as
+    it: the first files of the corpus (<= io_bytes) are written to a scratch
+    directory, then ii_map_files reads them (pipelined pread into pinned
+    windows + async H2D, `threads` readers) and maps them.  Page cache warm
+    (the files were just written); best of 2."""
+    import numpy as np
+    nf = 0
+    while nf < len(off) - 1 and off[nf + 1] <= io_bytes:
+        nf += 1
+    if nf == 0:
+        return None
+    td = tempfile.mkdtemp(prefix="ii_io_")
+    try:
+        paths = []
+        for f in range(nf):
+            p = os.path.join(td, "f%05d.txt" % f)
+            np.asarray(text[int(off[f]):int(off[f + 1])]).tofile(p)
+            paths.append(p)
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            idx.map_files(paths, nthreads=threads)
+            wall = time.perf_counter() - t0
+            st = idx.stats()
+            if best is None or wall < best[0]:
+                best = (wall, st.io_ms, st.io_bytes, st.ms_map)
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+    wall, io_ms, io_b, map_ms = best
+    return {"files": nf, "bytes": int(off[nf]), "threads": threads, "read_upload_ms": round(io_ms, 2),
+            "read_upload_GBps": round(io_b / (io_ms * 1e-3) / 1e9, 2) if io_ms > 0 else None,
+            "map_files_ms": round(wall * 1e3, 2), "map_files_GBps": round(int(off[nf]) / wall / 1e9, 2),
+            "k1_ms": round(map_ms, 2), "page_cache": "warm"}
 
 
 def main():
@@ -215,6 +253,7 @@ def main():
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_achieved = ph_bytes / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(text, off, a.cpu_sample_bytes)
+        io = io_leg(idx, text, off, a.io_bytes) if world == 1 and a.io_bytes > 0 else None
         line = {
             "metric": "indexed input GB/s (whole node) + % of HBM peak BW",
             "value": round(value, 3),
@@ -251,6 +290,7 @@ def main():
                                                    "achieved": round(st.sort0_bytes / (st.sort0_ms * 1e-3) / 1e9, 1)
                                                    if st.sort0_ms > 0 else 0.0}},
             "cpu_baseline": cpu,
+            "io": io,
             "phases_ms": {k: round(getattr(st, k), 3) for k in
                           ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total",
                            "emit_ms", "resolve_ms"]},

@@ -84,6 +84,11 @@ typedef struct {
     uint64_t resolved_tokens; /* tokens K1b handed to K1c (general path, full hot bucket, raced claim) */
     double sort0_ms;       /* first token-sort pass: dedup + lexid remap + compaction (k_sort0_compact) */
     uint64_t sort0_bytes;  /* its algorithmic bytes: 8 B per record read + 8 B per kept record written */
+    /* ii_map_files only (0 otherwise): host wall time of reading the files and
+     * uploading them (pipelined pread -> pinned windows -> async H2D), and
+     * the bytes uploaded */
+    double io_ms;
+    uint64_t io_bytes;
 } ii_stats;
 
 /* Open a context on HIP device `device`. */
@@ -101,7 +106,11 @@ const char *ii_strerror(int code);
  * Files must be given in ascending id0 order.  Missing / unreadable files are
  * reported on stderr in the reference's wording (main.c:98) and contribute
  * nothing; they are not an error.  `nthreads` host reader threads (the
- * reference's M) read the files.
+ * reference's M, at most 16) read the files: files[f].size (the stat size)
+ * fixes each file's place on the device, the threads pread 8 MiB windows
+ * into pinned buffers and upload each with an async copy on their own stream
+ * while reading the next.  A file found longer than its
+ * size makes the call fall back to whole-file reads.
  */
 int ii_map_files(ii_ctx *ctx, const ii_file *files, uint32_t nfiles, int nthreads,
                  uint64_t hist_out[II_ALPHABET]);
@@ -177,6 +186,24 @@ int ii_import(ii_ctx *ctx, int nparts, const void *d_recv, const uint64_t *recv_
 
 /* Text of <letter>.txt (letter 0..25 = 'a'..'z'), valid until the next call. */
 int ii_letter_text(ii_ctx *ctx, int letter, const char **buf, size_t *len);
+
+/*
+ * Partial files.  The reference's mappers write every kept
+ * token as "<clean word> <id0+1>\n" to partial_<first letter>.txt
+ * (main.c:113-118; files created at main.c:332-341).  The index does not need
+ * them; this builds their text on the device from the mapped input (valid
+ * after any ii_map_* call, until the next one; not after ii_import).
+ * order[0..n) lists indices of the mapped files (0 = first file of the map
+ * call) in emission order; tokens keep their text order inside each file.
+ * With the size order of ii_partition and M = 1 the text is byte-identical to
+ * the reference's; with M > 1 the reference interleaves mappers by thread
+ * timing, and the order given here (mapper 0's files, then mapper 1's, ...)
+ * is one of its outcomes.
+ */
+int ii_partials(ii_ctx *ctx, const uint32_t *order, uint32_t n);
+/* Text of partial_<letter>.txt after ii_partials, valid until the next map or
+ * ii_partials call. */
+int ii_partial_text(ii_ctx *ctx, int letter, const char **buf, size_t *len);
 
 /* Counters and phase timings of the last map + reduce. */
 int ii_get_stats(ii_ctx *ctx, ii_stats *out);

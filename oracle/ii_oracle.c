@@ -122,8 +122,10 @@ static void or_dict_add(or_dict *d, const char *w, uint32_t n, uint32_t id1) {
     d->slot[s] = ++d->n;
 }
 
-/* Tokenize one file's bytes (mapper hot loop, main.c:102-118). */
-static void or_map_bytes(or_dict dicts[OR_ALPHA], const unsigned char *p, uint64_t len, uint32_t id1) {
+/* Tokenize one file's bytes (mapper hot loop, main.c:102-118): emit(ctx,
+ * clean word, letters) for every token that keeps a letter. */
+typedef void (*or_emit_fn)(void *ctx, const char *w, uint32_t n, uint32_t id1);
+static void or_tokens(const unsigned char *p, uint64_t len, uint32_t id1, or_emit_fn emit, void *ctx) {
     char clean[OR_MAX_WORD];
     uint64_t i = 0;
     while (i < len) {
@@ -140,8 +142,17 @@ static void or_map_bytes(or_dict dicts[OR_ALPHA], const unsigned char *p, uint64
             else if (c >= 'a' && c <= 'z') clean[j++] = (char)c;
             if (j >= OR_MAX_WORD - 1) stopped = 1;
         }
-        if (j > 0) or_dict_add(&dicts[clean[0] - 'a'], clean, j, id1);
+        if (j > 0) emit(ctx, clean, j, id1); /* main.c:113 */
     }
+}
+
+static void or_emit_dict(void *ctx, const char *w, uint32_t n, uint32_t id1) {
+    or_dict *dicts = ctx;
+    or_dict_add(&dicts[w[0] - 'a'], w, n, id1); /* bucket by first letter, main.c:114-116 */
+}
+
+static void or_map_bytes(or_dict dicts[OR_ALPHA], const unsigned char *p, uint64_t len, uint32_t id1) {
+    or_tokens(p, len, id1, or_emit_dict, dicts);
 }
 
 static int or_cmp(const void *a, const void *b) {
@@ -224,6 +235,50 @@ int ii_oracle_index(const unsigned char *text, const uint64_t *file_off, const u
 }
 
 void ii_oracle_free(void *p) { free(p); }
+
+/* Partial files (main.c:113-118, format "%s %d\n" at main.c:116): one growing
+ * buffer per letter. */
+typedef struct { char *b; uint64_t n, cap; } or_buf;
+static void or_emit_partial(void *ctx, const char *w, uint32_t n, uint32_t id1) {
+    or_buf *pb = &((or_buf *)ctx)[w[0] - 'a'];
+    if (pb->n + n + 16 > pb->cap) {
+        pb->cap = (pb->cap + n + 16) * 2;
+        pb->b = realloc(pb->b, pb->cap);
+    }
+    memcpy(pb->b + pb->n, w, n);
+    pb->n += n;
+    pb->n += (uint64_t)sprintf(pb->b + pb->n, " %u\n", id1);
+}
+
+/*
+ * Text of the 26 partial_<letter>.txt files when one mapper reads the files
+ * order[0..norder) one after another (main.c:93-124): lines in token order.
+ * Same buffer convention as ii_oracle_index.
+ */
+int ii_oracle_partials(const unsigned char *text, const uint64_t *file_off, const uint32_t *file_id0,
+                       uint32_t nfiles, const uint32_t *order, uint32_t norder, char **out,
+                       uint64_t letter_off[OR_ALPHA + 1]) {
+    or_buf bufs[OR_ALPHA];
+    memset(bufs, 0, sizeof(bufs));
+    for (uint32_t i = 0; i < norder; i++) {
+        uint32_t f = order[i];
+        if (f >= nfiles) return -1;
+        or_tokens(text + file_off[f], file_off[f + 1] - file_off[f], file_id0[f] + 1, or_emit_partial, bufs);
+    }
+    uint64_t total = 0;
+    for (int l = 0; l < OR_ALPHA; l++) total += bufs[l].n;
+    char *buf = malloc(total + 1);
+    uint64_t o = 0;
+    for (int l = 0; l < OR_ALPHA; l++) {
+        letter_off[l] = o;
+        if (bufs[l].n) memcpy(buf + o, bufs[l].b, bufs[l].n);
+        o += bufs[l].n;
+        free(bufs[l].b);
+    }
+    letter_off[OR_ALPHA] = o;
+    *out = buf;
+    return 0;
+}
 
 #ifdef II_ORACLE_MAIN
 /* Same CLI as the reference: <num_mappers> <num_reducers> <input_file_list>

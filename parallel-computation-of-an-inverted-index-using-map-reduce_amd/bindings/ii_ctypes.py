@@ -37,6 +37,7 @@ class Stats(ctypes.Structure):
         ("emit_ms", ctypes.c_double), ("emit_bytes", ctypes.c_uint64), ("resolve_ms", ctypes.c_double),
         ("resolved_tokens", ctypes.c_uint64),
         ("sort0_ms", ctypes.c_double), ("sort0_bytes", ctypes.c_uint64),
+        ("io_ms", ctypes.c_double), ("io_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -100,6 +101,9 @@ def lib():
         L.ii_letter_load.argtypes = [ctypes.c_void_p, u64p]
         L.ii_balanced_letters.argtypes = [u64p, ctypes.c_int, i32p, i32p]
         L.ii_export_plan_ranges.argtypes = [ctypes.c_void_p, ctypes.c_int, i32p, i32p, u64p]
+        L.ii_partials.argtypes = [ctypes.c_void_p, u32p, ctypes.c_uint32]
+        L.ii_partial_text.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                      ctypes.POINTER(ctypes.c_size_t)]
         _lib = L
     return _lib
 
@@ -153,13 +157,17 @@ class Index:
                                    len(file_id0), hist), "ii_map_device")
         return list(hist)
 
-    def map_files(self, paths, nthreads=4, id0=None):
+    def map_files(self, paths, nthreads=4, id0=None, sizes=None):
+        """ii_map_files; `sizes` overrides the stat sizes (tests of the
+        reader's short-file padding and grown-file fallback)."""
         files = (IIFile * max(1, len(paths)))()
         keep = []
         for i, p in enumerate(paths):
             b = os.fsencode(p)
             keep.append(b)
             size = os.path.getsize(p) if os.path.exists(p) else 0
+            if sizes is not None:
+                size = sizes[i]
             files[i] = IIFile(b, size, i if id0 is None else id0[i])
         hist = (ctypes.c_uint64 * ALPHABET)()
         _check(lib().ii_map_files(self.h, files, len(paths), nthreads, hist), "ii_map_files")
@@ -202,6 +210,19 @@ class Index:
 
     def letters(self):
         return {chr(97 + l): self.letter_text(l) for l in range(ALPHABET)}
+
+    def partials(self, order):
+        """Text of the 26 partial_<letter>.txt files (ii_partials): `order`
+        lists indices of the mapped files in emission order."""
+        order = list(order)
+        _check(lib().ii_partials(self.h, _u32(order) if order else None, len(order)), "ii_partials")
+        out = {}
+        for l in range(ALPHABET):
+            buf = ctypes.c_char_p()
+            n = ctypes.c_size_t()
+            _check(lib().ii_partial_text(self.h, l, ctypes.byref(buf), ctypes.byref(n)), "ii_partial_text")
+            out[chr(97 + l)] = ctypes.string_at(buf, n.value) if n.value else b""
+        return out
 
     def stats(self):
         s = Stats()

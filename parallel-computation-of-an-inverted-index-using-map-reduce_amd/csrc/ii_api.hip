@@ -7,12 +7,16 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <vector>
 
 #include "../../include/ii.h"
 #include "ii_kernels.h"
+#include "ii_partial.h"
 
 using namespace ii;
 
@@ -38,6 +42,8 @@ struct ii_ctx {
     uint32_t nfiles = 0;
     uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df and the id sort bits)
     DBuf fstart, fid;
+    std::vector<uint64_t> h_fstart;  // host copies of the mapped files' starts / ids
+    std::vector<uint32_t> h_fid;
 
     // scratch
     DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable, kept;
@@ -52,6 +58,12 @@ struct ii_ctx {
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
     DBuf uniq, pstart, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    // partial-file emitter (ii_partials)
+    DBuf ppieces, pcnt, pout, ploff;
+    std::vector<char> part_host;
+    uint64_t h_part_off[II_ALPHABET + 1] = {0};
+    bool part_valid = false;
+    bool text_is_input = false;  // c->text holds mapped input files (not an imported word arena)
     // exchange
     DBuf woff, pts;
     uint64_t h_pts[3 * (II_ALPHABET + 1)] = {0};
@@ -80,6 +92,12 @@ struct ii_ctx {
     uint64_t n_pending = 0; // tokens K1b left to K1c
     uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
     uint64_t nch_map = 0;   // K1b chunks of the last map
+    // pipelined file reader (ii_map_files): per thread a stream and two pinned windows
+    std::vector<hipStream_t> io_st;
+    std::vector<uint8_t*> io_buf;
+    std::vector<hipEvent_t> io_ev;
+    double io_ms = 0;       // host wall time of the last ii_map_files read + upload
+    uint64_t io_bytes = 0;
     ii_stats stats;
 };
 
@@ -124,6 +142,11 @@ static T* P_(DBuf& b) {
 }
 
 static inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kBlock - 1) / kBlock); }
+static inline double now_ms() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
 static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 
 // ----------------------------------------------------------------- scan / sort
@@ -338,7 +361,8 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->llen,     &c->lstart, &c->tied,  &c->tpos,    &c->rid,    &c->rfirst,   &c->tdict,
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
-                   &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept};
+                   &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
+                   &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -351,6 +375,10 @@ extern "C" void ii_close(ii_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_c0)
         if (e) (void)hipEventDestroy(e);
+    for (auto s : c->io_st) (void)hipStreamSynchronize(s);
+    for (auto s : c->io_st) (void)hipStreamDestroy(s);
+    for (auto e : c->io_ev) (void)hipEventDestroy(e);
+    for (auto b : c->io_buf) (void)hipHostFree(b);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
@@ -523,6 +551,10 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
     }
     c->nfiles = nfiles;
     c->id_bound = nfiles ? file_id0[nfiles - 1] + 1 : 0;
+    c->h_fstart.assign(file_start, file_start + nfiles);
+    c->h_fid.assign(file_id0, file_id0 + nfiles);
+    c->part_valid = false;
+    c->text_is_input = true;
     return II_OK;
 }
 
@@ -545,6 +577,8 @@ extern "C" int ii_map_host(ii_ctx* c, const uint8_t* text, const uint64_t* file_
                            uint32_t nfiles, uint64_t hist_out[II_ALPHABET]) {
     if (!c || (nfiles && (!file_off || !file_id0 || !text))) return II_ERR_ARG;
     HIPCK(hipSetDevice(c->dev));
+    c->io_ms = 0;
+    c->io_bytes = 0;
     for (uint32_t f = 0; f < nfiles; f++)
         if (file_off[f + 1] < file_off[f]) return II_ERR_ARG;
     uint64_t total = nfiles ? file_off[nfiles] - file_off[0] + nfiles : 0;
@@ -567,7 +601,120 @@ extern "C" int ii_map_host(ii_ctx* c, const uint8_t* text, const uint64_t* file_
     return map_core(c, hist_out);
 }
 
+// ----------------------------------------------------------------- file reader (§8 f2)
+// ii_map_files replaces the mappers' fopen/fscanf (main.c:93-102) with a
+// pipelined reader: the device layout is known from the stat sizes (file f at
+// off[f], one '\n' separator after every file), the layout is cut into
+// windows of kIoWin bytes, and each of up to kIoThreads host threads reads
+// its windows (pread straight into one of its two pinned buffers) and hands
+// each one to its own stream as an async H2D copy, so reading window k+1
+// overlaps copying window k.  A file shorter than its stat size is padded
+// with spaces (no tokens); a file that turns out longer than its stat size
+// (grown, or a size the caller did not know) makes the call fall back to
+// whole-file reads (read_all_then_map).
 namespace {
+constexpr uint64_t kIoWin = 8ull << 20;
+constexpr int kIoThreads = 16;
+
+struct IoJob {
+    ii_ctx* c;
+    const ii_file* files;
+    uint32_t nfiles;
+    const uint64_t* off;  // nfiles + 1: device offset of every file (+1 separator each)
+    uint8_t* d_text;
+    uint64_t total, nwin;
+    int nt;
+    int err;      // first error (II_*), 0 = ok
+    int grown;    // some file had more bytes than its stat size
+    pthread_mutex_t mu;
+};
+struct IoArg {
+    IoJob* j;
+    int t;
+};
+
+// Fill window [lo, hi) of the device layout into buf.
+static void io_fill(IoJob* j, uint64_t lo, uint64_t hi, uint8_t* buf) {
+    uint32_t f = (uint32_t)(std::upper_bound(j->off, j->off + j->nfiles + 1, lo) - j->off) - 1;
+    for (; f < j->nfiles && j->off[f] < hi; f++) {
+        const uint64_t fsz = j->off[f + 1] - j->off[f] - 1;  // bytes of file f (separator excluded)
+        const uint64_t a = std::max(lo, j->off[f]), b = std::min(hi, j->off[f] + fsz);
+        if (b > a || (fsz == 0 && j->off[f] >= lo)) {
+            // every window that holds file bytes (or the separator of an empty file) opens it;
+            // only the window holding the file's first byte reports a failure (main.c:98)
+            const int fd = open(j->files[f].path, O_RDONLY);
+            const bool first = j->off[f] >= lo;
+            if (fd < 0) {
+                if (first) fprintf(stderr, "Mapper %d: Error opening file %s\n", 0, j->files[f].path);
+                if (b > a) memset(buf + (a - lo), ' ', b - a);
+            } else {
+                uint64_t done = 0;
+                while (a + done < b) {
+                    const ssize_t r = pread(fd, buf + (a + done - lo), b - a - done, (off_t)(a + done - j->off[f]));
+                    if (r <= 0) break;
+                    done += (uint64_t)r;
+                }
+                if (a + done < b) memset(buf + (a + done - lo), ' ', b - a - done);  // shorter than stat: spaces
+                if (j->off[f] + fsz <= hi) {  // this window holds the file's end: is there more?
+                    uint8_t extra;
+                    if (pread(fd, &extra, 1, (off_t)fsz) == 1) {
+                        pthread_mutex_lock(&j->mu);
+                        j->grown = 1;
+                        pthread_mutex_unlock(&j->mu);
+                    }
+                }
+                close(fd);
+            }
+        }
+        const uint64_t sep = j->off[f] + fsz;  // separator byte of file f
+        if (sep >= lo && sep < hi) buf[sep - lo] = '\n';
+    }
+}
+
+static void* io_worker(void* p) {
+    IoArg* a = (IoArg*)p;
+    IoJob* j = a->j;
+    ii_ctx* c = j->c;
+    int err = II_OK;
+    if (hipSetDevice(c->dev) != hipSuccess) err = II_ERR_HIP;
+    int k = 0;
+    for (uint64_t w = (uint64_t)a->t; err == II_OK && w < j->nwin; w += (uint64_t)j->nt, k ^= 1) {
+        const int b = 2 * a->t + k;
+        if (hipEventSynchronize(c->io_ev[b]) != hipSuccess) { err = II_ERR_HIP; break; }  // buffer free again
+        const uint64_t lo = w * kIoWin, hi = std::min(j->total, lo + kIoWin);
+        io_fill(j, lo, hi, c->io_buf[b]);
+        if (hipMemcpyAsync(j->d_text + lo, c->io_buf[b], hi - lo, hipMemcpyHostToDevice, c->io_st[a->t]) != hipSuccess ||
+            hipEventRecord(c->io_ev[b], c->io_st[a->t]) != hipSuccess)
+            err = II_ERR_HIP;
+    }
+    if (err == II_OK && hipStreamSynchronize(c->io_st[a->t]) != hipSuccess) err = II_ERR_HIP;
+    if (err != II_OK) {
+        pthread_mutex_lock(&j->mu);
+        if (!j->err) j->err = err;
+        pthread_mutex_unlock(&j->mu);
+    }
+    return nullptr;
+}
+
+static int io_setup(ii_ctx* c, int nt) {
+    while ((int)c->io_st.size() < nt) {
+        hipStream_t s;
+        HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        c->io_st.push_back(s);
+        for (int k = 0; k < 2; k++) {
+            void* h = nullptr;
+            hipEvent_t e;
+            HIPCK(hipHostMalloc(&h, kIoWin, hipHostMallocDefault));
+            HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCK(hipEventRecord(e, s));  // the first wait on it returns at once
+            c->io_buf.push_back((uint8_t*)h);
+            c->io_ev.push_back(e);
+        }
+    }
+    return II_OK;
+}
+
+// Whole-file reads, then one copy (files whose size was not known up front).
 struct ReadJob {
     const ii_file* files;
     uint32_t n;
@@ -588,7 +735,7 @@ void* read_worker(void* arg) {
             continue;
         }
         std::vector<uint8_t>& d = (*j->data)[f];
-        d.resize(j->files[f].size ? j->files[f].size : 4096);
+        d.resize(j->files[f].size ? j->files[f].size + 1 : 4096);
         size_t len = 0, r;
         while ((r = fread(d.data() + len, 1, d.size() - len, fp)) > 0) {
             len += r;
@@ -601,9 +748,8 @@ void* read_worker(void* arg) {
 }
 }  // namespace
 
-extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, int nthreads,
-                            uint64_t hist_out[II_ALPHABET]) {
-    if (!c || (nfiles && !files)) return II_ERR_ARG;
+static int read_all_then_map(ii_ctx* c, const ii_file* files, uint32_t nfiles, int nthreads,
+                             uint64_t hist_out[II_ALPHABET]) {
     std::vector<std::vector<uint8_t>> data(nfiles);
     ReadJob job{files, nfiles, &data, 0, PTHREAD_MUTEX_INITIALIZER};
     int nt = std::max(1, std::min(nthreads, 64));
@@ -621,6 +767,41 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
         if (!data[f].empty()) memcpy(text.data() + off[f], data[f].data(), data[f].size());
     data.clear();
     return ii_map_host(c, text.data(), off.data(), ids.data(), nfiles, hist_out);
+}
+
+extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, int nthreads,
+                            uint64_t hist_out[II_ALPHABET]) {
+    if (!c || (nfiles && !files)) return II_ERR_ARG;
+    for (uint32_t f = 0; f < nfiles; f++)
+        if (!files[f].path || (f && files[f].id0 <= files[f - 1].id0)) return II_ERR_ARG;
+    HIPCK(hipSetDevice(c->dev));
+    const double t0 = now_ms();
+    std::vector<uint64_t> off(nfiles + 1, 0);
+    for (uint32_t f = 0; f < nfiles; f++) off[f + 1] = off[f] + files[f].size + 1;
+    const uint64_t total = off[nfiles];
+    CK(grow(c->text_own, std::max<uint64_t>(total, 16)));
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nthreads, 1), (uint64_t)kIoThreads,
+                                                                    (total + kIoWin - 1) / kIoWin}));
+    CK(io_setup(c, nt));
+    IoJob job{c, files, nfiles, off.data(), P_<uint8_t>(c->text_own), total, (total + kIoWin - 1) / kIoWin, nt, 0, 0,
+              PTHREAD_MUTEX_INITIALIZER};
+    std::vector<pthread_t> th(nt);
+    std::vector<IoArg> args(nt);
+    for (int t = 0; t < nt; t++) {
+        args[t] = IoArg{&job, t};
+        pthread_create(&th[t], nullptr, io_worker, &args[t]);
+    }
+    for (int t = 0; t < nt; t++) pthread_join(th[t], nullptr);
+    if (job.err) return job.err;
+    if (job.grown) return read_all_then_map(c, files, nfiles, nthreads, hist_out);
+    c->io_ms = now_ms() - t0;
+    c->io_bytes = total;
+    c->text = P_<uint8_t>(c->text_own);
+    c->nbytes = total;
+    std::vector<uint32_t> ids(nfiles);
+    for (uint32_t f = 0; f < nfiles; f++) ids[f] = files[f].id0;
+    CK(set_files(c, off.data(), ids.data(), nfiles));
+    return map_core(c, hist_out);
 }
 
 // ----------------------------------------------------------------- reduce
@@ -953,6 +1134,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     const uint64_t fs0 = 0;
     const uint32_t id0 = 0;
     CK(set_files(c, &fs0, &id0, A ? 1 : 0));
+    c->text_is_input = false;
     CK(map_core(c, nullptr, true));  // tokenises the words: word k -> rec[k] = slot << 32
     if (c->T != W) return II_ERR_INTERNAL;
     c->id_bound = id_bound;
@@ -998,6 +1180,60 @@ extern "C" int ii_letter_text(ii_ctx* c, int letter, const char** buf, size_t* l
     static const char empty[1] = {0};
     uint64_t a = c->h_letter_off[letter], b = c->h_letter_off[letter + 1];
     *buf = c->host_text.empty() ? empty : c->host_text.data() + a;
+    *len = (size_t)(b - a);
+    return II_OK;
+}
+
+// ----------------------------------------------------------------- partial files (§8 f3)
+extern "C" int ii_partials(ii_ctx* c, const uint32_t* order, uint32_t n) {
+    if (!c || (n && !order)) return II_ERR_ARG;
+    if (!c->mapped || !c->text_is_input) return II_ERR_STATE;
+    HIPCK(hipSetDevice(c->dev));
+    c->part_valid = false;
+    std::vector<PartPiece> pieces;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t f = order[i];
+        if (f >= c->nfiles) return II_ERR_ARG;
+        const uint64_t lo = c->h_fstart[f], hi = f + 1 < c->nfiles ? c->h_fstart[f + 1] : c->nbytes;
+        for (uint64_t a = lo; a < hi; a += kPartPiece)
+            pieces.push_back(PartPiece{a, std::min(hi, a + kPartPiece), c->h_fid[f], 0});
+    }
+    const uint64_t np = pieces.size();
+    if (np > 0xFFFFFFFFull) return II_ERR_ARG;
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    CK(grow(c->ploff, sizeof(uint64_t) * (II_ALPHABET + 1)));
+    uint64_t* ploff = P_<uint64_t>(c->ploff);
+    uint64_t total = 0;
+    if (np) {
+        CK(grow(c->ppieces, sizeof(PartPiece) * np));
+        CK(grow(c->pcnt, sizeof(uint64_t) * 26 * np));
+        HIPCK(hipMemcpyAsync(c->ppieces.p, pieces.data(), sizeof(PartPiece) * np, hipMemcpyHostToDevice, c->st));
+        const PartPiece* dp = P_<PartPiece>(c->ppieces);
+        uint64_t* cnt = P_<uint64_t>(c->pcnt);
+        k_part_count<<<(uint32_t)np, kBlock, 0, c->st>>>(c->text, c->nbytes, dp, (uint32_t)np, cnt);
+        CK(run_scan(c, OpInPlace{cnt}, 26 * np, totals));
+        CK(read_u64(c, totals, &total));
+        CK(grow(c->pout, std::max<uint64_t>(total, 16)));
+        k_part_write<<<(uint32_t)np, kBlock, 0, c->st>>>(c->text, c->nbytes, dp, (uint32_t)np, cnt,
+                                                       P_<uint8_t>(c->pout));
+        k_part_letter_off<<<1, 64, 0, c->st>>>(cnt, (uint32_t)np, totals, ploff);
+        HIPCK(hipGetLastError());
+        CK(read_u64(c, ploff, c->h_part_off, II_ALPHABET + 1));
+    } else {
+        memset(c->h_part_off, 0, sizeof(c->h_part_off));
+    }
+    c->part_host.resize(total + 1);
+    if (total) HIPCK(hipMemcpyAsync(c->part_host.data(), c->pout.p, total, hipMemcpyDeviceToHost, c->st));
+    HIPCK(hipStreamSynchronize(c->st));
+    c->part_valid = true;
+    return II_OK;
+}
+
+extern "C" int ii_partial_text(ii_ctx* c, int letter, const char** buf, size_t* len) {
+    if (!c || letter < 0 || letter >= II_ALPHABET || !buf || !len) return II_ERR_ARG;
+    if (!c->part_valid) return II_ERR_STATE;
+    const uint64_t a = c->h_part_off[letter], b = c->h_part_off[letter + 1];
+    *buf = c->part_host.data() + a;
     *len = (size_t)(b - a);
     return II_OK;
 }
@@ -1063,6 +1299,8 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
             s.sort0_bytes = c->c0_bytes;
         }
     }
+    s.io_ms = c->io_ms;
+    s.io_bytes = c->io_bytes;
     *o = s;
     return II_OK;
 }

@@ -8,6 +8,13 @@
  * The map and reduce phases (main.c:326-384) run on the MI355X through
  * libii.so (include/ii.h); M sizes the host reader threads and R the writer
  * threads, neither changes the output.
+ *
+ * With II_PARTIAL_FILES=1 in the environment the CLI also leaves the
+ * reference's partial_<letter>.txt files in the current directory
+ * (main.c:332-341, lines "<word> <id>\n" written at main.c:116), mapper m's
+ * files (size order, main.c:300-323) after mapper m-1's: byte-identical to
+ * the reference's for M = 1.  Off by default: the index
+ * does not need them.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -102,6 +109,30 @@ int main(int argc, char **argv) {
     }
     /* files in list (= ID) order: postings come out ascending (main.c:217-226) */
     rc = ii_map_files(ctx, files, (uint32_t)count, M, NULL);
+    const char *pe = getenv("II_PARTIAL_FILES");
+    if (rc == II_OK && pe && atoi(pe) == 1) {
+        /* mapper m reads order[sb[m] .. se[m]) (main.c:93); mappers one after another */
+        uint32_t n = 0;
+        for (int m = 0; m < M; m++)
+            for (uint32_t i = sb[m]; i < se[m]; i++) order[n++] = order[i];
+        rc = ii_partials(ctx, order, n);
+        for (int l = 0; rc == II_OK && l < 26; l++) {
+            const char *buf;
+            size_t len;
+            char name[32];
+            snprintf(name, sizeof(name), "partial_%c.txt", 'a' + l);
+            rc = ii_partial_text(ctx, l, &buf, &len);
+            if (rc != II_OK) break;
+            FILE *o = fopen(name, "w+");
+            if (!o) {
+                fprintf(stderr, "Error creating partial file: %s\n", name); /* main.c:336 */
+                rc = II_ERR_IO;
+                break;
+            }
+            if (len && fwrite(buf, 1, len, o) != len) rc = II_ERR_IO;
+            fclose(o);
+        }
+    }
     if (rc == II_OK) rc = ii_reduce(ctx, 1);
     if (rc != II_OK) {
         fprintf(stderr, "ii_index: %s\n", ii_strerror(rc));

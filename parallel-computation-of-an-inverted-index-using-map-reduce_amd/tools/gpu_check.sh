@@ -41,6 +41,6 @@ timeout -k 10 480 python bench.py --steps "$STEPS" --warmup 2 --bytes "$BYTES" >
 tail -1 "$OUT/bench.log" && \
 echo "== rocprof" && \
 timeout -k 10 480 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 1 --bytes "$BYTES" --no-cpu-baseline > "$OUT/prof.log" 2>&1 && \
+    python3 bench.py --steps "$STEPS" --warmup 1 --bytes "$BYTES" --no-cpu-baseline --io-bytes 0 > "$OUT/prof.log" 2>&1 && \
 tail -1 "$OUT/prof.log" && \
 find "$OUT/prof" -name '*kernel_stats.csv' -exec head -16 {} \;

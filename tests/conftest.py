@@ -78,3 +78,20 @@ def case_arrays(name):
 
 
 CASES = ["config1", "config2", "edge", "rand_0", "rand_1", "rand_2", "tiny360", "zipf_small"]
+
+
+def partials_meta():
+    """tests/golden/partials.json: the reference's partial files, M = 1."""
+    import json
+    return json.load(open(os.path.join(GOLDEN, "partials.json")))["cases"]
+
+
+def size_order(case):
+    """Files in the reference's one-mapper read order (main.c:300: size
+    descending; glibc's qsort is a stable merge sort, so ties keep list order;
+    a missing file has size 0, main.c:294)."""
+    list_text, files, _ = load_case(case)
+    toks = list_text.split()
+    paths = toks[1:1 + int(toks[0])]
+    sizes = [len(files[p]) if p in files else 0 for p in paths]
+    return sorted(range(len(paths)), key=lambda i: (-sizes[i], i))

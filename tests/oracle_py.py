@@ -15,6 +15,9 @@ def _load():
         _lib.ii_oracle_index.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
         _lib.ii_oracle_free.argtypes = [ctypes.c_void_p]
+        _lib.ii_oracle_partials.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.c_void_p]
     return _lib
 
 
@@ -32,6 +35,28 @@ def oracle_index(text, file_off, file_id0):
     loff = (ctypes.c_uint64 * 27)()
     rc = L.ii_oracle_index(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
                            ctypes.byref(out), loff)
+    assert rc == 0
+    res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
+    L.ii_oracle_free(out)
+    return res
+
+
+def oracle_partials(text, file_off, file_id0, order):
+    """-> {letter: bytes} of partial_<letter>.txt when one mapper reads the
+    files `order` (indices) one after another (main.c:93-124)."""
+    import numpy as np
+    L = _load()
+    if hasattr(text, "ctypes"):
+        tb = np.ascontiguousarray(text, dtype=np.uint8)
+    else:
+        tb = np.frombuffer(bytes(text), dtype=np.uint8)
+    off = np.ascontiguousarray(np.asarray(file_off, dtype=np.uint64))
+    ids = np.ascontiguousarray(np.asarray(file_id0, dtype=np.uint32))
+    od = np.ascontiguousarray(np.asarray(list(order), dtype=np.uint32))
+    out = ctypes.c_void_p()
+    loff = (ctypes.c_uint64 * 27)()
+    rc = L.ii_oracle_partials(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
+                              od.ctypes.data if od.size else None, len(od), ctypes.byref(out), loff)
     assert rc == 0
     res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
     L.ii_oracle_free(out)

@@ -8,8 +8,8 @@ import tempfile
 
 import pytest
 
-from conftest import CASES, GOLDEN, ORACLE, case_arrays, materialize
-from oracle_py import oracle_index
+from conftest import CASES, GOLDEN, ORACLE, case_arrays, load_case, materialize, partials_meta, size_order
+from oracle_py import oracle_index, oracle_partials
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -50,3 +50,24 @@ def test_oracle_defined_ub_long_token():
     got = oracle_index(text, [0, len(text)], [0])
     assert got["a"] == b"a" * 299 + b":[1]\n"
     assert got["b"] == b"b:[1]\n"
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_partials_match_reference(case):
+    # the reference's partial_<l>.txt with M = 1 (tests/golden/make_partial_golden.py)
+    text, off, ids, _ = case_arrays(case)
+    got = oracle_partials(text, off, ids, size_order(case))
+    meta = partials_meta()[case]
+    for l in "abcdefghijklmnopqrstuvwxyz":
+        assert hashlib.sha256(got[l]).hexdigest() == meta[l]["sha256"], "partial_%s.txt differs" % l
+
+
+def test_partition_order_is_size_order():
+    import ii_ctypes
+    for case in CASES:
+        list_text, files, _ = load_case(case)
+        toks = list_text.split()
+        paths = toks[1:1 + int(toks[0])]
+        sizes = [len(files[p]) if p in files else 0 for p in paths]
+        order, sb, se = ii_ctypes.partition(sizes, 1)
+        assert order == size_order(case) and (sb[0], se[0]) == (0, len(paths))
