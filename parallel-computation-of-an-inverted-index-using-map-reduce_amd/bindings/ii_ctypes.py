@@ -70,7 +70,9 @@ def lib():
     global _lib
     if _lib is None:
         _init_torch_first()
-        path = os.path.join(PKG_DIR, "libii.so")
+        # II_LIB_VARIANT=x loads libii_x.so (A/B builds of kernel variants, tools/gpu_ab.sh)
+        var = os.environ.get("II_LIB_VARIANT")
+        path = os.path.join(PKG_DIR, "libii_%s.so" % var if var else "libii.so")
         if not os.path.exists(path):
             raise FileNotFoundError("libii.so not built (make -C %s)" % PKG_DIR)
         L = ctypes.CDLL(path)

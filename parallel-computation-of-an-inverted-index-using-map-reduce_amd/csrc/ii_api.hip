@@ -264,8 +264,8 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, *v, *v2, n, chunk, shift, db,
                                                                       (uint32_t)nch, table, nullptr);
         else
-            k_radix_scatter<false><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, nullptr, nullptr, n, chunk, shift, db,
-                                                                       (uint32_t)nch, table, first0 ? kept : nullptr);
+            k_radix_scatter<false, II_SC_NT, II_SC_IT><<<(uint32_t)nch, II_SC_NT, 0, c->st>>>(
+                src, dst, nullptr, nullptr, n, chunk, shift, db, (uint32_t)nch, table, first0 ? kept : nullptr);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
             c->n_sc++;
@@ -529,7 +529,8 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(read_u64(c, totals, &c->T));
         CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
     }
-    k_hist_reduce<<<26, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
+    HIPCK(hipMemsetAsync(counters + C_HIST, 0, sizeof(uint64_t) * II_ALPHABET, c->st));
+    k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
     HIPCK(hipGetLastError());
     CK(read_u64(c, counters + C_HIST, c->hist, II_ALPHABET));
     if (hist_out) memcpy(hist_out, c->hist, sizeof(c->hist));

@@ -1005,14 +1005,23 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
+// Per-letter totals of the per-chunk letter counts (chunk_hist[c * 26 + l]).
+// kHistThreads is a multiple of 26, so every thread strides over one letter's
+// column (coalesced across the grid), then one LDS and one global add per
+// letter and workgroup; counters[C_HIST ..] must be zero on entry.
+constexpr uint32_t kHistBlocks = 416;  // 416 * 256 = 26 * 4096 threads
 __global__ __launch_bounds__(kBlock) void k_hist_reduce(const uint32_t* __restrict__ chunk_hist, uint64_t nch,
                                                         uint64_t* __restrict__ counters) {
-    __shared__ uint64_t s_scan[kWaves + 1];
+    __shared__ unsigned long long s[26];
+    if (threadIdx.x < 26) s[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)kHistBlocks * kBlock, n = nch * 26;
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     uint64_t acc = 0;
-    for (uint64_t c = threadIdx.x; c < nch; c += kBlock) acc += chunk_hist[c * 26 + blockIdx.x];
-    uint64_t tot;
-    (void)block_excl_scan(acc, &tot, s_scan);
-    if (threadIdx.x == 0) counters[C_HIST + blockIdx.x] = tot;
+    for (uint64_t e = g; e < n; e += stride) acc += chunk_hist[e];
+    atomicAdd(&s[g % 26], (unsigned long long)acc);
+    __syncthreads();
+    if (threadIdx.x < 26) atomicAdd((unsigned long long*)&counters[C_HIST + threadIdx.x], s[threadIdx.x]);
 }
 
 // number of occupied word-table slots
@@ -1276,6 +1285,9 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
 // voff[c0], the range pass 0's scatter reads back.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+#ifndef II_S0_TTS
+#define II_S0_TTS 0
+#endif
 constexpr int kCBlock = 512;                    // 8 waves share one 64 KiB dedup bitmap
 constexpr int kCWaves = kCBlock / 64;
 constexpr int kCTile = kSortItems * kCBlock;    // records per tile
@@ -1357,7 +1369,13 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             const uint64_t slot = raw[k] >> 32;
             if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
                 const uint32_t bit = 1u << (slot & 31);
+#if II_S0_TTS
+                // test before set: a slot already seen in this epoch is dropped
+                // with a plain LDS read; only first sightings pay the atomic
+                ok = !(bm[slot >> 5] & bit) && !(atomicOr(&bm[slot >> 5], bit) & bit);
+#else
                 ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
+#endif
             }
             const uint64_t b = __ballot(ok);
             pos[k] = wcount + (uint32_t)__popcll(b & lt);

@@ -161,6 +161,15 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortItems = 16;                     // keys per thread per tile
 constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
+#ifndef II_SC_NT
+#define II_SC_NT 512  // threads per workgroup of the token-sort scatter (tile = II_SC_NT * II_SC_IT keys; 512 x 16 measured best: 1.95 ms vs 2.22 for 256, 2.39 for 1024, 2.66 for 512 x 24 at 10 GB)
+#endif
+#ifndef II_SC_IT
+#define II_SC_IT 16  // keys per thread per tile of the token-sort scatter
+#endif
+#ifndef II_SC_PF
+#define II_SC_PF 0  // 1: the scatter issues the next tile's loads before ranking this one
+#endif
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).  Same
@@ -202,55 +211,69 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 // compacted ranges k_sort0_compact leaves — instead of [b*chunk, (b+1)*chunk).
 // dbits <= kRadixBits: digit width of this pass (fewer buckets -> longer runs
 // per tile -> better coalesced stores).
-template <bool kHasVals>
-__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
-                                                          const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
-                                                          uint64_t n, uint64_t chunk, int shift, int dbits,
-                                                          uint32_t nchunks, const uint64_t* __restrict__ table,
-                                                          const uint64_t* __restrict__ kept) {
-    __shared__ uint64_t s_keys[kSortTile];
-    __shared__ uint32_t s_vals[kHasVals ? kSortTile : 1];
-    __shared__ uint32_t s_wcnt[kWaves][kRadix];
+// NT threads per workgroup: a tile holds NT * kSortItems keys, so with
+// NT = 512 every digit's output run is twice as long as with 256 (the store
+// side is what bounds the pass: 6-bit passes, with twice the run length of
+// 7-bit ones, run ~15 % faster).  Threads t < kRadix own one digit each.
+template <bool kHasVals, int NT = kBlock, int IT = kSortItems>
+__global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                      const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
+                                                      uint64_t n, uint64_t chunk, int shift, int dbits,
+                                                      uint32_t nchunks, const uint64_t* __restrict__ table,
+                                                      const uint64_t* __restrict__ kept) {
+    constexpr int NW = NT / 64;
+    constexpr int kTileN = NT * IT;
+    constexpr int kDW = kRadix / 64;  // waves that own digits
+    static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
+    __shared__ uint64_t s_keys[kTileN];
+    __shared__ uint32_t s_vals[kHasVals ? kTileN : 1];
+    __shared__ uint32_t s_wcnt[NW][kRadix];
     __shared__ uint32_t s_tstart[kRadix];
     __shared__ uint64_t s_run[kRadix];
-    __shared__ uint64_t s_scan[kWaves + 1];
-    static_assert(kRadix == kBlock, "one digit per thread");
+    __shared__ uint64_t s_scan[kDW];
 
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
+    const bool digit_thread = t < kRadix;
     const uint32_t dmask = (1u << dbits) - 1u;
     const uint64_t lo = kept ? kept[kMaxChunks + blockIdx.x] : (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = kept ? lo + kept[blockIdx.x] : (lo + chunk < n ? lo + chunk : n);
-    s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
+    if (digit_thread) s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
     const uint64_t lt = lanemask_lt();
 
     // the next tile's keys are loaded while this tile is ranked and written
-    uint64_t nkey[kSortItems];
-    uint32_t nval[kSortItems];
+    uint64_t nkey[IT];
+    uint32_t nval[IT];
     auto load_tile = [&](uint64_t tb) {
-        const uint64_t wb = tb + (uint64_t)w * 64 * kSortItems + l;
+        const uint64_t wb = tb + (uint64_t)w * 64 * IT + l;
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < IT; k++) {
             const uint64_t idx = wb + (uint64_t)k * 64;
             nkey[k] = idx < hi ? kin[idx] : ~0ull;
             if (kHasVals) nval[k] = idx < hi ? vin[idx] : 0u;
         }
     };
     if (lo < hi) load_tile(lo);
-    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
+    uint32_t tot_d = 0;
+    for (uint64_t tb = lo; tb < hi; tb += kTileN) {
+        if (digit_thread) {
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ww++) s_wcnt[ww][t] = 0;
-        uint64_t key[kSortItems];
-        uint32_t val[kSortItems];
-        uint32_t rank[kSortItems];
-        const uint64_t wbase = tb + (uint64_t)w * 64 * kSortItems + l;
+            for (int ww = 0; ww < NW; ww++) s_wcnt[ww][t] = 0;
+        }
+        uint64_t key[IT];
+        uint32_t val[IT];
+        uint32_t rank[IT];
+        const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < IT; k++) {
             key[k] = nkey[k];
             if (kHasVals) val[k] = nval[k];
         }
+#if II_SC_PF
+        if (tb + kTileN < hi) load_tile(tb + kTileN);
+#endif
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < IT; k++) {
             const bool valid = wbase + (uint64_t)k * 64 < hi;
             const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
             uint64_t m = __ballot(valid);
@@ -272,18 +295,37 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
         }
         __syncthreads();
         // digit t: totals, tile start, per-wave offsets
-        uint32_t c0 = s_wcnt[0][t], c1 = s_wcnt[1][t], c2 = s_wcnt[2][t], c3 = s_wcnt[3][t];
-        uint32_t tot_d = c0 + c1 + c2 + c3;
-        uint64_t all;
-        uint32_t start = (uint32_t)block_excl_scan(tot_d, &all, s_scan);
-        s_tstart[t] = start;
-        s_wcnt[0][t] = start;
-        s_wcnt[1][t] = start + c0;
-        s_wcnt[2][t] = start + c0 + c1;
-        s_wcnt[3][t] = start + c0 + c1 + c2;
+        uint32_t cw[NW];
+        tot_d = 0;
+        if (digit_thread) {
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                cw[ww] = s_wcnt[ww][t];
+                tot_d += cw[ww];
+            }
+        }
+        const uint64_t inc = wave_incl_scan(tot_d);
+        if (w < kDW && l == 63) s_scan[w] = inc;
+        __syncthreads();
+        uint64_t wb = 0, all = 0;
+#pragma unroll
+        for (int ww = 0; ww < kDW; ww++) {
+            const uint64_t sv = s_scan[ww];
+            if (ww < w) wb += sv;
+            all += sv;
+        }
+        if (digit_thread) {
+            uint32_t run = (uint32_t)(wb + inc - tot_d);
+            s_tstart[t] = run;
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                s_wcnt[ww][t] = run;
+                run += cw[ww];
+            }
+        }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < IT; k++) {
             if (wbase + (uint64_t)k * 64 < hi) {
                 const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
                 const uint32_t pos = s_wcnt[w][d] + rank[k];
@@ -292,11 +334,13 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
             }
         }
         __syncthreads();
-        if (tb + kSortTile < hi) load_tile(tb + kSortTile);
+#if !II_SC_PF
+        if (tb + kTileN < hi) load_tile(tb + kTileN);
+#endif
         const uint32_t tile_n = (uint32_t)all;
 #pragma unroll
-        for (int j = 0; j < kSortItems; j++) {
-            const uint32_t p = j * kBlock + t;
+        for (int j = 0; j < IT; j++) {
+            const uint32_t p = j * NT + t;
             if (p < tile_n) {
                 const uint64_t k = s_keys[p];
                 const uint32_t d = (uint32_t)(k >> shift) & dmask;
@@ -306,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
             }
         }
         __syncthreads();
-        s_run[t] += tot_d;
+        if (digit_thread) s_run[t] += tot_d;
         // the next iteration's first __syncthreads orders this update before use
     }
 }
