@@ -48,7 +48,7 @@ struct ii_ctx {
     // scratch
     DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable, kept;
     // K1
-    DBuf rec, rec2, longs, pend, pend_cnt;
+    DBuf rec, rec2, longs, pend, pend_cnt, chunk_files;
     DBuf tkeys, trep;
     uint64_t big_cap = 1ull << 22;  // big word table; total slots = kHotSlots + big_cap
     uint64_t long_cap = 0;
@@ -362,7 +362,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
-                   &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff};
+                   &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -468,6 +468,9 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
     }
     CK(grow(c->pend_cnt, sizeof(uint32_t) * nch));
+    CK(grow(c->chunk_files, sizeof(uint32_t) * 3 * nch));
+    k_chunk_files<<<grid_for(nch), kBlock, 0, c->st>>>(fstart, fid, c->nfiles, c->nbytes, kChunk, nch,
+                                                      P_<uint32_t>(c->chunk_files));
     const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;  // the long queue grows on overflow
     if (c->long_cap < std::max<uint64_t>(1 << 16, t_est / 64)) c->long_cap = std::max<uint64_t>(1 << 16, t_est / 64);
 
@@ -485,12 +488,13 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
                                                        c->rec_cap, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                       P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt));
+                                                       P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
+                                                       P_<uint32_t>(c->chunk_files));
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         k_tok_resolve<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
                                                            c->rec_cap, P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
                                                            P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                           P_<LongTok>(c->longs), c->long_cap);
+                                                           P_<LongTok>(c->longs), c->long_cap, P_<uint32_t>(c->chunk_files));
         HIPCK(hipEventRecord(c->ev_res[1], c->st));
         CK(run_reduce(c, OpU32{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());

@@ -238,6 +238,24 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ start, 
     return f_lo;
 }
 
+// Per K1 chunk c: {first file, last file, id0 of the first file} — one
+// binary search per chunk for the whole grid, instead of a serial search by
+// one thread at the start of every K1b / K1c workgroup (~28 dependent loads
+// in each workgroup's critical path).
+__global__ __launch_bounds__(kBlock) void k_chunk_files(const uint64_t* __restrict__ file_start,
+                                                        const uint32_t* __restrict__ file_id, uint32_t nfiles,
+                                                        uint64_t nbytes, uint64_t chunk, uint64_t nch,
+                                                        uint32_t* __restrict__ cf) {
+    const uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= nch) return;
+    const uint64_t lo = c * chunk, hi = lo + chunk < nbytes ? lo + chunk : nbytes;
+    const uint32_t f0 = file_of(file_start, 0, nfiles - 1, lo);
+    const uint32_t f1 = file_of(file_start, f0, nfiles - 1, hi - 1);
+    cf[3 * c] = f0;
+    cf[3 * c + 1] = f1;
+    cf[3 * c + 2] = file_id[f0];
+}
+
 __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, uint64_t nbytes, int64_t g) {
     if (g >= 0 && (uint64_t)g + 16 <= nbytes) return *reinterpret_cast<const uint4*>(text + g);
     uint32_t w[4] = {0, 0, 0, 0};
@@ -797,7 +815,8 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
                                                      const uint32_t* __restrict__ file_id, uint32_t nfiles,
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                     uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt) {
+                                                     uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
+                                                     const uint32_t* __restrict__ cf) {
     __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kRoundStaged];
     __shared__ uint32_t s_mask[kRoundWins + 1];   // per window: terminator (ws | NUL) bits | letter bits << 16
     __shared__ uint16_t s_off[kMaxRoundTok];      // round-local start of every kept token, text order
@@ -810,12 +829,8 @@ __global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8
     const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
     if (t < 32) s_hist[t] = 0;
-    if (t == 0) {
-        s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
-        s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
-        s_f[2] = file_id[s_f[0]];
-        s_npend = 0;
-    }
+    if (t < 3) s_f[t] = cf[3 * (uint64_t)blockIdx.x + t];  // k_chunk_files
+    if (t == 0) s_npend = 0;
     const uint64_t cbase = chunk_base(chunk_off, cap);
     const uint32_t rot = chunk_rot(blockIdx.x);
     uint32_t out = 0;  // records emitted so far
@@ -942,7 +957,8 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
                                                         const uint32_t* __restrict__ pend,
                                                         const uint32_t* __restrict__ pend_cnt, Table tab,
                                                         uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                        LongTok* __restrict__ longs, uint64_t long_cap) {
+                                                        LongTok* __restrict__ longs, uint64_t long_cap,
+                                                        const uint32_t* __restrict__ cf) {
     __shared__ LongTok s_long[kLongBuf];
     __shared__ uint32_t s_hist[32];
     __shared__ uint32_t s_f[3];
@@ -952,14 +968,9 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
     if (n == 0) return;
     const int t = threadIdx.x;
     const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
-    const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
     if (t < 32) s_hist[t] = 0;
-    if (t == 0) {
-        s_f[0] = file_of(file_start, 0, nfiles - 1, chunk_lo);
-        s_f[1] = file_of(file_start, s_f[0], nfiles - 1, chunk_hi - 1);
-        s_f[2] = file_id[s_f[0]];
-        s_lcount = 0;
-    }
+    if (t < 3) s_f[t] = cf[3 * (uint64_t)blockIdx.x + t];  // k_chunk_files
+    if (t == 0) s_lcount = 0;
     __syncthreads();
     const uint64_t cbase = chunk_base(chunk_off, cap);
     const bool fsame = s_f[0] == s_f[1];
@@ -1285,12 +1296,22 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
 // voff[c0], the range pass 0's scatter reads back.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+#ifndef II_S0_DEFER
+#define II_S0_DEFER 0  // 1: a tile's kept records are stored one tile later (gathers overlap the next loads)
+#endif
 #ifndef II_S0_TTS
 #define II_S0_TTS 0
 #endif
-constexpr int kCBlock = 512;                    // 8 waves share one 64 KiB dedup bitmap
+#ifndef II_S0_NT
+#define II_S0_NT 512
+#endif
+#ifndef II_S0_IT
+#define II_S0_IT 16
+#endif
+constexpr int kCBlock = II_S0_NT;               // 8 waves share one 64 KiB dedup bitmap
+constexpr int kS0Items = II_S0_IT;              // records per thread per tile
 constexpr int kCWaves = kCBlock / 64;
-constexpr int kCTile = kSortItems * kCBlock;    // records per tile
+constexpr int kCTile = kS0Items * kCBlock;    // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
 // LDS: 8 KiB counts + 64 KiB bitmap + 4 KiB offsets, so two workgroups fit a CU
 
@@ -1312,7 +1333,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
     if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
     __syncthreads();
-    const uint64_t tofs = (uint64_t)w * 64 * kSortItems + l;
+    const uint64_t tofs = (uint64_t)w * 64 * kS0Items + l;
     const uint64_t lt = lanemask_lt();
     // this lane's chunk cursor (its indices only grow), all in registers so a
     // record's address needs no LDS round trip unless it enters a new chunk
@@ -1323,10 +1344,10 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint64_t o = lo;  // next output position
     // (prefetching the next tile, before or after the remap gathers, measured
     // slower: 5.3 -> 5.9-6.2 ms at 10 GB)
-    uint64_t nraw[kSortItems];
+    uint64_t nraw[kS0Items];
     auto load_tile = [&](uint64_t tb) {
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < kS0Items; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
             uint64_t src = idx;
             if (cap && idx < hi) {
@@ -1345,11 +1366,31 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             nraw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
         }
     };
+#if II_S0_DEFER
+    uint32_t p_fid[kS0Items], p_lex[kS0Items], p_pos[kS0Items];
+    uint32_t p_keep = 0;
+    uint64_t p_base = 0;
+    auto st_prev = [&]() {
+#pragma unroll
+        for (int k = 0; k < kS0Items; k++) {
+            if ((p_keep >> k) & 1u) {
+                const uint64_t r = ((uint64_t)p_lex[k] << 32) | p_fid[k];
+                st_nt(kout + p_base + p_pos[k], r);
+                atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
+            }
+        }
+    };
+#endif
     for (uint64_t tb = lo; tb < hi; tb += kCTile) {
         load_tile(tb);
-        uint64_t raw[kSortItems];
+#if II_S0_DEFER
+        // store the previous tile while this tile's loads are in flight: its
+        // remap gathers were issued one tile ago
+        st_prev();
+#endif
+        uint64_t raw[kS0Items];
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) raw[k] = nraw[k];
+        for (int k = 0; k < kS0Items; k++) raw[k] = nraw[k];
         if (threadIdx.x == 0) {  // thread 0's item 0 is the tile's first record
             const uint32_t f = (uint32_t)raw[0];
             s_flag = f != s_epoch;
@@ -1362,9 +1403,13 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         }
         const uint32_t epoch = s_epoch;
         uint32_t keep = 0, wcount = 0;
-        uint32_t pos[kSortItems];
+#if II_S0_DEFER
+        uint32_t (&pos)[kS0Items] = p_pos;  // the previous tile's positions are consumed by now
+#else
+        uint32_t pos[kS0Items];
+#endif
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
             if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
@@ -1382,9 +1427,32 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             wcount += (uint32_t)__popcll(b);
             keep |= (uint32_t)ok << k;
         }
+#if II_S0_DEFER
+#pragma unroll
+        for (int k = 0; k < kS0Items; k++) {  // this tile's gathers, consumed one tile later
+            p_fid[k] = (uint32_t)raw[k];
+            p_lex[k] = ((keep >> k) & 1u) ? remap[raw[k] >> 32] : 0u;
+        }
+        p_keep = keep;
+        if (l == 0) s_wtot[w] = wcount;
+        __syncthreads();
+        uint32_t wbase = 0, ttot = 0;
+#pragma unroll
+        for (int ww = 0; ww < kCWaves; ww++) {
+            const uint32_t c = s_wtot[ww];
+            if (ww < w) wbase += c;
+            ttot += c;
+        }
+        p_base = o + wbase;
+        o += ttot;
+        __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
+    }
+    st_prev();  // the last tile
+    __syncthreads();
+#else
         // the remap gathers of the kept records are in flight across the barrier
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++)  // slot -> lexicographic id, in place
+        for (int k = 0; k < kS0Items; k++)  // slot -> lexicographic id, in place
             if ((keep >> k) & 1u) raw[k] = ((uint64_t)remap[raw[k] >> 32] << 32) | (raw[k] & 0xFFFFFFFFull);
         if (l == 0) s_wtot[w] = wcount;
         __syncthreads();
@@ -1396,7 +1464,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             ttot += c;
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < kS0Items; k++) {
             if ((keep >> k) & 1u) {
                 const uint64_t r = raw[k];
                 st_nt(kout + o + wbase + pos[k], r);
@@ -1406,6 +1474,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         o += ttot;
         __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
     }
+#endif
     for (int d = threadIdx.x; d < kRadix; d += kCBlock) {
         uint32_t tt = 0;
 #pragma unroll

@@ -52,14 +52,17 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
           uint32_t* pend, uint32_t* pcnt) {
     hipEvent_t a, b, c;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); CK(hipEventCreate(&c));
+    uint32_t* cf;
+    CK(hipMalloc(&cf, 12 * nch));
+    k_chunk_files<<<(uint32_t)((nch + kBlock - 1) / kBlock), kBlock>>>(fstart, fid, nf, nb, kChunk, nch, cf);
     float best = 1e9;
     for (int it = 0; it < 4; it++) {
         CK(hipMemset(tab.keys, 0, nslots * 8));
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
-        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, tab, rec, chist, pend, pcnt);
+        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, tab, rec, chist, pend, pcnt, cf);
         CK(hipEventRecord(b));
-        k_tok_resolve<<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap);
+        k_tok_resolve<<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap, cf);
         CK(hipEventRecord(c));
         CK(hipEventSynchronize(c));
         float ms, ms2; CK(hipEventElapsedTime(&ms, a, b)); CK(hipEventElapsedTime(&ms2, b, c));
