@@ -57,7 +57,11 @@ struct ii_ctx {
     DBuf dslot, dkey, dkey2, didx, didx2, remap, lkey, lrep, llen, lstart;
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
-    DBuf uniq, pstart, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
+    DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
+    bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
+    uint64_t NW = 0;        // wid range
     // partial-file emitter (ii_partials)
     DBuf ppieces, pcnt, pout, ploff;
     std::vector<char> part_host;
@@ -210,7 +214,8 @@ struct OpInPlace {
 // kept ranges back into *k, and the remaining passes run over the kept
 // records only.  *n_out receives the number of records kept.
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
-                    bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr) {
+                    bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr,
+                    bool wid = false) {
     if (passes) *passes = 0;
     if (n_out) *n_out = n;
     if (hi <= lo || (n <= 1 && !remap0)) return II_OK;
@@ -248,9 +253,14 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-            k_sort0_compact<<<(uint32_t)nch, kCBlock, 0, c->st>>>(*k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in,
-                                                                 (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
-                                                                 table, remap0, *k2, kept);
+            if (wid)
+                k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
+                    *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
+                    (uint32_t)nch, table, remap0, *k2, kept);
+            else
+                k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
+                    *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
+                    (uint32_t)nch, table, remap0, *k2, kept);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
         } else {
@@ -274,7 +284,13 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         if (passes) (*passes)++;
         if (first0) {  // sorted by the first digit, in *k: the rest runs over the kept records
             const uint64_t n_in = n;
-            CK(read_u64(c, totals + 4, &n));
+            uint64_t t47[4];
+            CK(read_u64(c, totals + 4, t47, 4));
+            n = t47[0];
+            if (wid) {  // exact wid range (k_count_hot wrote the occupied hot slots to totals[7])
+                c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));
+                hi = std::min(hi, lo + std::max(1, bitlen(c->NW - 1)));
+            }
             c->c0_bytes = 8 * n_in + 8 * n;
             if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n;
             if (n_out) *n_out = n;
@@ -292,10 +308,12 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
 // K3: distinct (lexid, id0) pairs of the sorted records r[0, n), their
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
 // (post_start[V] = U).  Sets c->U.
-static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n) {
+static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false) {
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
     CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
+    CK(grow(c->pstop, sizeof(uint64_t) * (c->V + 1)));
+    uint64_t* pe = P_<uint64_t>(c->pstop);
     uint64_t* uniq = P_<uint64_t>(c->uniq);
     uint64_t* Pp = P_<uint64_t>(c->P);
     uint64_t* ps = P_<uint64_t>(c->pstart);
@@ -313,7 +331,18 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n) {
     k_uniq_reduce<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part);
     k_scan_partials<<<1, kBlock, 0, c->st>>>(part, (uint32_t)nch, ps + c->V);
     k_scan_partials<<<1, kBlock, 0, c->st>>>(part + kMaxChunks, (uint32_t)nch, totals + 6);
-    k_uniq_apply<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part, uniq, Pp, ps);
+    uint64_t* ps_k = ps;  // starts / ends by record key
+    uint64_t* pe_k = pe;
+    if (wid) {
+        CK(grow(c->pstart_w, sizeof(uint64_t) * (c->NW + 1)));
+        CK(grow(c->pstop_w, sizeof(uint64_t) * (c->NW + 1)));
+        ps_k = P_<uint64_t>(c->pstart_w);
+        pe_k = P_<uint64_t>(c->pstop_w);
+    }
+    k_uniq_apply<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part, uniq, Pp, ps_k, pe_k);
+    k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
+    if (wid)
+        k_wid_post<<<grid_for(c->V), kBlock, 0, c->st>>>(P_<uint32_t>(c->widl), (uint32_t)c->V, ps_k, pe_k, ps, pe);
     HIPCK(hipGetLastError());
     CK(read_u64(c, ps + c->V, &c->U));
     HIPCK(hipMemcpyAsync(Pp + c->U, totals + 6, sizeof(uint64_t), hipMemcpyDeviceToDevice, c->st));
@@ -362,7 +391,8 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->tk,       &c->tk2,    &c->tv,    &c->tv2,     &c->uniq,   &c->pstart,   &c->okey,
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
-                   &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files};
+                   &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
+                   &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -419,6 +449,7 @@ static bool use_fixed_capacity(ii_ctx* c, uint64_t nch, bool dense) {
 // dense: records of token k at rec[k] (the import path indexes them so)
 static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = false) {
     c->mapped = c->have_pairs = c->reduced = false;
+    c->wid_pairs = false;
     c->planned_parts = 0;
     c->host_valid = false;
     c->n_sc = 0;
@@ -810,7 +841,7 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
 }
 
 // ----------------------------------------------------------------- reduce
-static int build_dictionary(ii_ctx* c) {
+static int build_dictionary(ii_ctx* c, bool wid = false) {
     uint64_t* counters = P_<uint64_t>(c->counters);
     uint64_t* totals = P_<uint64_t>(c->totals);
     const uint32_t V = (uint32_t)c->V;
@@ -887,6 +918,18 @@ static int build_dictionary(ii_ctx* c) {
                                                    P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen));
     k_letter_start<<<grid_for(V + 1), kBlock, 0, c->st>>>(sk, V, P_<uint32_t>(c->lstart));
     HIPCK(hipGetLastError());
+    if (wid) {  // word ids of the single-GPU token sort (k_wid_finish)
+        CK(grow(c->wmap, sizeof(uint32_t) * nslots));
+        CK(grow(c->lexw, sizeof(uint32_t) * (kHotSlots + V)));
+        CK(grow(c->widl, sizeof(uint32_t) * (V + 1)));
+        uint32_t* nhot = reinterpret_cast<uint32_t*>(totals + 7);
+        HIPCK(hipMemsetAsync(totals + 7, 0, sizeof(uint64_t), c->st));
+        k_count_hot<<<grid_for(V), kBlock, 0, c->st>>>(dslot, V, nhot);
+        k_wid_finish<<<grid_for(V), kBlock, 0, c->st>>>(di, dslot, V, nhot, P_<uint32_t>(c->wmap),
+                                                       P_<uint32_t>(c->lexw), P_<uint32_t>(c->widl));
+        HIPCK(hipGetLastError());
+        c->NW = kHotSlots + V;  // bound; run_sort refines it from totals[7] after its first pass (no extra sync)
+    }
     // keep the sorted prefix keys in dkey for the order step
     if (sk != P_<uint64_t>(c->dkey)) std::swap(c->dkey, c->dkey2);
     return II_OK;
@@ -895,7 +938,9 @@ static int build_dictionary(ii_ctx* c) {
 // Local reduce: dictionary (lexicographic ids), K2 token sort, K3 unique
 // pairs.  After it the context holds a partial index: uniq (lexid, id0)
 // pairs grouped by word, post_start, and the per-word dictionary arrays.
-static int local_reduce(ii_ctx* c) {
+// wid: sort by word id (single-GPU reduce, k_wid_finish) instead of lexid;
+// the exchange path needs letter-contiguous pairs and sorts by lexid.
+static int local_reduce(ii_ctx* c, bool wid = false) {
     uint64_t* totals = P_<uint64_t>(c->totals);
     (void)totals;
     c->n_sc = 0;
@@ -908,21 +953,24 @@ static int local_reduce(ii_ctx* c) {
         return II_OK;
     }
     // ---- dictionary: lexicographic ids
-    CK(build_dictionary(c));
+    if (getenv("II_SORT_KEYS") && !strcmp(getenv("II_SORT_KEYS"), "lexid")) wid = false;
+    CK(build_dictionary(c, wid));
     HIPCK(hipEventRecord(c->ev[2], c->st));
 
     // ---- K2: sort records by (lexid, fid); fid order is kept by stability
     uint64_t* r = P_<uint64_t>(c->rec);
     uint64_t* r2 = P_<uint64_t>(c->rec2);
-    const int lb = std::max(1, bitlen(V - 1));
+    const int lb = std::max(1, bitlen((wid ? c->NW : V) - 1));
     uint64_t Tk = T;
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes, P_<uint32_t>(c->remap), &Tk));
+    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
+                P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid));
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
 
     // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
-    CK(run_unique(c, r, Tk));
+    CK(run_unique(c, r, Tk, wid));
+    c->wid_pairs = wid;
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;
     c->have_pairs = true;
@@ -955,7 +1003,8 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     uint32_t* ov = P_<uint32_t>(c->oval);
     uint32_t* ov2 = P_<uint32_t>(c->oval2);
     const int dbits = std::max(1, bitlen(c->id_bound));
-    k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, (uint32_t)V, dbits, ok, ov);
+    uint64_t* pe = P_<uint64_t>(c->pstop);
+    k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, pe, (uint32_t)V, dbits, ok, ov);
     CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr));
     c->ord = ov;
     HIPCK(hipEventRecord(c->ev[5], c->st));
@@ -965,14 +1014,16 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     CK(grow(c->letter_off, sizeof(uint64_t) * (II_ALPHABET + 1)));
     uint64_t* Pp = P_<uint64_t>(c->P);
     uint64_t* loff = P_<uint64_t>(c->loff);
-    CK(run_scan(c, OpLineOff{ov, P_<uint32_t>(c->llen), ps, Pp, loff}, V, totals + 2));
+    CK(run_scan(c, OpLineOff{ov, P_<uint32_t>(c->llen), ps, pe, Pp, loff}, V, totals + 2));
     CK(read_u64(c, totals + 2, &c->out_bytes));
     CK(grow(c->out, std::max<uint64_t>(c->out_bytes, 16)));
     uint8_t* out = P_<uint8_t>(c->out);
+    CK(grow(c->fbase, sizeof(uint64_t) * (c->wid_pairs ? c->NW : V)));
+    uint64_t* fb = P_<uint64_t>(c->fbase);
     k_fmt_words<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
-                                                  P_<uint32_t>(c->llen), ps, Pp, loff, (uint32_t)V, out);
-    k_fmt_posts<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(uniq, c->U, P_<uint32_t>(c->llen),
-                                                                                          ps, Pp, loff, out);
+                                                  P_<uint32_t>(c->llen), ps, pe, Pp, loff, (uint32_t)V, out,
+                                                  c->wid_pairs ? P_<uint32_t>(c->widl) : nullptr, fb);
+    k_fmt_posts<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(uniq, c->U, fb, Pp, out);
     k_letter_off<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), ov, loff, (uint32_t)V, c->out_bytes,
                                       P_<uint64_t>(c->letter_off));
     HIPCK(hipGetLastError());
@@ -1002,7 +1053,7 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     if (!c) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c));
+    if (!c->have_pairs) CK(local_reduce(c, true));
     return order_and_format(c, copy_text);
 }
 
@@ -1010,6 +1061,7 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
 // Per-letter points of the partial index (first word / pair / arena byte).
 static int letter_points(ii_ctx* c) {
     const uint64_t V = c->V;
+    if (c->wid_pairs) return II_ERR_STATE;  // after ii_reduce: the exchange needs ii_reduce_local first
     if (V == 0 || c->T == 0) {
         memset(c->h_pts, 0, sizeof(c->h_pts));
         return II_OK;

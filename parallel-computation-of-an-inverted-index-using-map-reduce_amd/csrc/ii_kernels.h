@@ -1242,6 +1242,34 @@ __global__ __launch_bounds__(kBlock) void k_tie_place(const uint64_t* __restrict
 }
 
 // Per lexicographic id j: remap[slot] = j, the word's key / occurrence / length.
+// Word ids for the single-GPU token sort ("wid" keys).  The token sort only
+// has to GROUP each word's records (ids ascending); lexicographic order is
+// needed per word, not per record.  So records are sorted by a word id that
+// costs no gather for hot-table words: wid = the hot slot itself, and for a
+// big-table word kHotSlots + its rank among the occupied big slots.  K3 maps
+// wid -> lexid once per distinct pair, where consecutive records share the
+// word (a coalesced broadcast), instead of sort0 gathering remap[slot] for
+// every kept record in text order (random, one L2 request per lane).
+// nhot = number of occupied hot slots (dict_slot ascends): *nhot must be 0 on entry.
+__global__ __launch_bounds__(kBlock) void k_count_hot(const uint32_t* __restrict__ dict_slot, uint32_t V,
+                                                      uint32_t* __restrict__ nhot) {
+    const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
+    if (d < V && dict_slot[d] < kHotSlots && (d + 1 == V || dict_slot[d + 1] >= kHotSlots)) *nhot = d + 1;
+}
+// per lexid j: wid(j); lexw[wid] = j, wmap[slot] = wid for big-table slots
+__global__ __launch_bounds__(kBlock) void k_wid_finish(const uint32_t* __restrict__ dict_idx,
+                                                       const uint32_t* __restrict__ dict_slot, uint32_t V,
+                                                       const uint32_t* __restrict__ nhot, uint32_t* __restrict__ wmap,
+                                                       uint32_t* __restrict__ lexw, uint32_t* __restrict__ widl) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= V) return;
+    const uint32_t d = dict_idx[j], s = dict_slot[d];
+    const uint32_t wid = s < kHotSlots ? s : (uint32_t)kHotSlots + (d - *nhot);
+    lexw[wid] = j;
+    widl[j] = wid;
+    if (s >= kHotSlots) wmap[s] = wid;
+}
+
 __global__ __launch_bounds__(kBlock) void k_lex_finish(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                        const uint32_t* __restrict__ dict_idx,
                                                        const uint32_t* __restrict__ dict_slot,
@@ -1315,6 +1343,7 @@ constexpr int kCTile = kS0Items * kCBlock;    // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
 // LDS: 8 KiB counts + 64 KiB bitmap + 4 KiB offsets, so two workgroups fit a CU
 
+template <bool kWid>
 __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
                                                            const uint64_t* __restrict__ voff, uint32_t nch_in,
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
@@ -1431,7 +1460,9 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {  // this tile's gathers, consumed one tile later
             p_fid[k] = (uint32_t)raw[k];
-            p_lex[k] = ((keep >> k) & 1u) ? remap[raw[k] >> 32] : 0u;
+            p_lex[k] = ((keep >> k) & 1u) ? ((kWid && (raw[k] >> 32) < kHotSlots) ? (uint32_t)(raw[k] >> 32)
+                                                                                   : remap[raw[k] >> 32])
+                                          : 0u;
         }
         p_keep = keep;
         if (l == 0) s_wtot[w] = wcount;
@@ -1453,7 +1484,12 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         // the remap gathers of the kept records are in flight across the barrier
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)  // slot -> lexicographic id, in place
-            if ((keep >> k) & 1u) raw[k] = ((uint64_t)remap[raw[k] >> 32] << 32) | (raw[k] & 0xFFFFFFFFull);
+            if ((keep >> k) & 1u) {
+                const uint32_t slot = (uint32_t)(raw[k] >> 32);
+                // wid keys: only big-table words need the map (remap = wmap)
+                const uint32_t key = (kWid && slot < kHotSlots) ? slot : remap[slot];
+                raw[k] = ((uint64_t)key << 32) | (raw[k] & 0xFFFFFFFFull);
+            }
         if (l == 0) s_wtot[w] = wcount;
         __syncthreads();
         uint32_t wbase = 0, ttot = 0;
@@ -1585,9 +1621,13 @@ __global__ __launch_bounds__(kBlock) void k_uniq_reduce(const uint64_t* __restri
     }
 }
 
+// Records are keyed by wid or lexid; uniq pairs keep the key, post_start[key]
+// = the word's first pair, post_end[key] = one past its last (the last word's
+// end is set by k_post_last; wid-keyed starts/ends go to lexids in k_wid_post).
 __global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restrict__ rec, uint64_t n, uint64_t chunk,
                                                        const uint64_t* __restrict__ part, uint64_t* __restrict__ uniq,
-                                                       uint64_t* __restrict__ P, uint64_t* __restrict__ post_start) {
+                                                       uint64_t* __restrict__ P, uint64_t* __restrict__ post_start,
+                                                       uint64_t* __restrict__ post_end) {
     __shared__ uint64_t lds[2 * kWaves];
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint64_t run_c = part[blockIdx.x], run_b = part[kMaxChunks + blockIdx.x];
@@ -1607,10 +1647,14 @@ __global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restric
         for (int q = 0; q < kUniqItems; q++) {
             if ((c >> (16 * q)) & 1ull) {
                 const uint64_t u = rc + ((ec >> (16 * q)) & 0xFFFFull);
+                const uint32_t key = (uint32_t)(r[q] >> 32);
                 uniq[u] = r[q];
                 P[u] = rb + ((eb >> (16 * q)) & 0xFFFFull);
                 const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
-                if (i == 0 || (r[q] >> 32) != (pv[q] >> 32)) post_start[r[q] >> 32] = u;
+                if (i == 0 || key != (uint32_t)(pv[q] >> 32)) {
+                    post_start[key] = u;
+                    if (i > 0) post_end[(uint32_t)(pv[q] >> 32)] = u;
+                }
             }
             rc += (tc >> (16 * q)) & 0xFFFFull;
             rb += (tb >> (16 * q)) & 0xFFFFull;
@@ -1620,15 +1664,32 @@ __global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restric
     }
 }
 
+// post_end of the last word = U (= post_start[V], written by the scan)
+__global__ void k_post_last(const uint64_t* __restrict__ rec, uint64_t n, const uint64_t* __restrict__ U,
+                            uint64_t* __restrict__ post_end) {
+    if (threadIdx.x == 0 && n) post_end[(uint32_t)(rec[n - 1] >> 32)] = *U;
+}
+// wid-keyed word starts / ends -> lexid-indexed ones (V threads)
+__global__ __launch_bounds__(kBlock) void k_wid_post(const uint32_t* __restrict__ widl, uint32_t V,
+                                                     const uint64_t* __restrict__ ps_w, const uint64_t* __restrict__ pe_w,
+                                                     uint64_t* __restrict__ ps, uint64_t* __restrict__ pe) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= V) return;
+    const uint32_t w = widl[j];
+    ps[j] = ps_w[w];
+    pe[j] = pe_w[w];
+}
+
 // ---------------------------------------------------------------- K4 order
 // key = letter << dbits | (dmax - df): ascending == (letter, df desc); the
 // stable sort keeps lexicographic order among equal df (main.c:55-64).
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ post_start,
+                                                       const uint64_t* __restrict__ post_end,
                                                        uint32_t V, int dbits, uint64_t* __restrict__ okey,
                                                        uint32_t* __restrict__ oval) {
     uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= V) return;
-    uint64_t df = post_start[j + 1] - post_start[j];
+    uint64_t df = post_end[j] - post_start[j];
     uint64_t dmax = (1ull << dbits) - 1;
     uint64_t letter = (sk[j] >> 59) - 1;
     okey[j] = (letter << dbits) | (dmax - df);
@@ -1654,11 +1715,12 @@ struct OpLineOff {
     const uint32_t* ord;
     const uint32_t* lex_len;
     const uint64_t* post_start;
+    const uint64_t* post_end;
     const uint64_t* P;
     uint64_t* loff;  // by lexid
     __device__ uint64_t value(uint64_t i) const {
         uint32_t w = ord[i];
-        return (uint64_t)lex_len[w] + 3 + (P[post_start[w + 1]] - P[post_start[w]]);
+        return (uint64_t)lex_len[w] + 3 + (P[post_end[w]] - P[post_start[w]]);
     }
     __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { loff[ord[i]] = ex; }
 };
@@ -1666,28 +1728,32 @@ struct OpLineOff {
 __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                       const uint64_t* __restrict__ lex_key, const uint64_t* __restrict__ lex_rep,
                                                       const uint32_t* __restrict__ lex_len,
-                                                      const uint64_t* __restrict__ post_start, const uint64_t* __restrict__ P,
-                                                      const uint64_t* __restrict__ loff, uint32_t V, uint8_t* __restrict__ out) {
+                                                      const uint64_t* __restrict__ post_start,
+                                                      const uint64_t* __restrict__ post_end, const uint64_t* __restrict__ P,
+                                                      const uint64_t* __restrict__ loff, uint32_t V, uint8_t* __restrict__ out,
+                                                      const uint32_t* __restrict__ widl, uint64_t* __restrict__ fbase) {
     uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= V) return;
     uint64_t o = loff[j];
     uint32_t len = lex_len[j];
+    // posting p of word j starts at fbase[key(j)] + P[p] (key = wid or lexid):
+    // one gather per posting in k_fmt_posts instead of four
+    fbase[widl ? widl[j] : j] = o + len + 2 - P[post_start[j]];
     write_word(text, nbytes, lex_key[j], lex_rep[j], len, out + o);
     out[o + len] = ':';
     out[o + len + 1] = '[';
-    out[o + len + 3 + (P[post_start[j + 1]] - P[post_start[j]]) - 1] = '\n';
+    out[o + len + 3 + (P[post_end[j]] - P[post_start[j]]) - 1] = '\n';
 }
 
+// uniq keys are wids or lexids, fbase is indexed the same way (k_fmt_words)
 __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
-                                                      const uint32_t* __restrict__ lex_len,
-                                                      const uint64_t* __restrict__ post_start, const uint64_t* __restrict__ P,
-                                                      const uint64_t* __restrict__ loff, uint8_t* __restrict__ out) {
+                                                      const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
+                                                      uint8_t* __restrict__ out) {
     for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < U; p += (uint64_t)gridDim.x * kBlock) {
         uint64_t r = uniq[p];
         uint32_t w = (uint32_t)(r >> 32);
         const uint64_t id = (r & 0xFFFFFFFFull) + 1;
-        const uint64_t ps = post_start[w];
-        const uint64_t o = loff[w] + lex_len[w] + 2 + (P[p] - P[ps]);
+        const uint64_t o = fbase[w] + P[p];
         const uint32_t nd = id_digits(id);
         if (id <= 0xFFFFFFFFull) {
             uint32_t v = (uint32_t)id;
@@ -1702,7 +1768,8 @@ __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict
                 v /= 10u;
             }
         }
-        out[o + nd] = (p + 1 == post_start[w + 1]) ? ']' : ' ';
+        // last posting of the word: the next pair belongs to another word (runs are contiguous)
+        out[o + nd] = (p + 1 == U || (uint32_t)(uniq[p + 1] >> 32) != w) ? ']' : ' ';
     }
 }
 
