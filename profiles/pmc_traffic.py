@@ -9,8 +9,9 @@ alone, then WRITE_SIZE alone: they cannot share a pass on gfx950), each under
 `timeout -s KILL`.  `summarize` averages the counters per dispatch of every
 kernel and applies the gfx950 correction: FETCH_SIZE counts half the bytes of
 a wide (16 B/lane) streaming read, so the read side is calibrated on
-k_tok_count, whose read bytes are known (the text, B bytes, read once with
-16-B loads); WRITE_SIZE is taken as reported.
+k_tok_count when the run has it (its read bytes are known: the text, B bytes,
+read once with 16-B loads; measured factor 1.93), else doubled as the guide
+prescribes (II_PMC_FETCH_FACTOR overrides); WRITE_SIZE is taken as reported.
 """
 import csv
 import collections
@@ -59,13 +60,13 @@ def summarize(out):
         if line.startswith("{"):
             meta = json.loads(line)
     B = meta.get("config", {}).get("bytes_per_rank")
-    factor = None
+    factor = float(os.environ.get("II_PMC_FETCH_FACTOR", "2.0"))
     if B and "ii::k_tok_count" in res and "FETCH_SIZE" in res["ii::k_tok_count"]:
         known = B
         factor = known / (res["ii::k_tok_count"]["FETCH_SIZE"] * 1024)
     for name, v in res.items():
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            rd = v["FETCH_SIZE"] * 1024 * (factor or 1.0)
+            rd = v["FETCH_SIZE"] * 1024 * factor
             v["read_bytes_per_launch"] = rd
             v["write_bytes_per_launch"] = v["WRITE_SIZE"] * 1024
             v["traffic_bytes_per_launch"] = rd + v["WRITE_SIZE"] * 1024
