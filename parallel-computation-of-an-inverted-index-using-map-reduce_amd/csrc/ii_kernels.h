@@ -65,7 +65,10 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 //              bucket was already full.
 // A word lives in exactly one place: a probe scans the same bucket (then the
 // same big-table run) in the same order and slots only go empty -> full.
-constexpr int kHotLog2 = 19;
+#ifndef II_HOT_LOG2
+#define II_HOT_LOG2 19
+#endif
+constexpr int kHotLog2 = II_HOT_LOG2;  // hot level: 2^19 slots (4 MB of keys) in 8-slot buckets
 constexpr uint64_t kHotSlots = 1ull << kHotLog2;
 constexpr int kBucket = 8;
 
@@ -560,10 +563,10 @@ __device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint64_t cap, uint3
 // (chunk_hist = the partial_<letter>.txt line counts); tokens of > 12 letters
 // are queued for the hash-collision check.
 #ifndef II_K1_WIN
-#define II_K1_WIN 4
+#define II_K1_WIN 2  // 8 KiB rounds: half the LDS, 6 waves/SIMD (emit 14.5 -> 13.95 ms at 10 GB vs 16 KiB rounds)
 #endif
 #ifndef II_K1_MINWAVES
-#define II_K1_MINWAVES 4
+#define II_K1_MINWAVES 6
 #endif
 constexpr int kWin = II_K1_WIN;                  // 16-B windows per lane per round
 constexpr int kRound = kWin * 16 * kBlock;       // 16 KiB of text per round
@@ -1323,7 +1326,10 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // layout or at i in the dense one (cap == 0).  Its kept records go to
 // kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
 // voff[c0], the range pass 0's scatter reads back.
-constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+// the dedup bitmap covers the first 2^19 hot slots (64 KiB of LDS): two
+// workgroups per CU; with a larger hot level the rest is not deduplicated
+constexpr uint64_t kDedupSlots = kHotSlots < (1ull << 19) ? kHotSlots : (1ull << 19);
+constexpr uint32_t kDedupWords = (uint32_t)(kDedupSlots / 32);
 #ifndef II_S0_DEFER
 #define II_S0_DEFER 0  // 1: a tile's kept records are stored one tile later (gathers overlap the next loads)
 #endif
@@ -1441,7 +1447,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
-            if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
+            if (ok && slot < kDedupSlots && (uint32_t)raw[k] == epoch) {
                 const uint32_t bit = 1u << (slot & 31);
 #if II_S0_TTS
                 // test before set: a slot already seen in this epoch is dropped
