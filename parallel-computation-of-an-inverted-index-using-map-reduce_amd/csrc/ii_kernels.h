@@ -57,18 +57,21 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 // read is corrected by the CAS.
 //
 // Two levels, one slot space:
-//   hot table  slots [0, 2^17): 8-slot buckets (one 64-B line), probed inside
-//              the bucket only.  Words that arrive first — in a Zipf corpus
-//              mostly the frequent ones — fill it; 1 MB of keys stays in every
-//              XCD's 4 MB L2, so most probes never leave L2.
-//   big table  slots [2^17, 2^17 + cap): linear probing; words whose hot
-//              bucket was already full.
+//   hot table  slots [0, kHotSlots = 2^20): 8-slot buckets (one 64-B line),
+//              probed inside the bucket only.  Words that arrive first — in a
+//              Zipf corpus mostly the frequent ones — fill it; the probes of
+//              frequent words hit L2, the rest the Infinity Cache (8 MB of
+//              keys).  K1b resolves hot words itself; words that overflow to
+//              the big table go to K1c (2^19 slots: 7.8 % of tokens, 2^20: less,
+//              K1c 5.1 -> 3.4 ms at 10 GB).
+//   big table  slots [kHotSlots, kHotSlots + cap): linear probing; words
+//              whose hot bucket was already full.
 // A word lives in exactly one place: a probe scans the same bucket (then the
 // same big-table run) in the same order and slots only go empty -> full.
 #ifndef II_HOT_LOG2
-#define II_HOT_LOG2 19
+#define II_HOT_LOG2 20  // 2^20: K1c 5.1 -> 3.4 ms at 10 GB vs 2^19 (fewer words overflow to the big table)
 #endif
-constexpr int kHotLog2 = II_HOT_LOG2;  // hot level: 2^19 slots (4 MB of keys) in 8-slot buckets
+constexpr int kHotLog2 = II_HOT_LOG2;  // hot level: 2^20 slots (8 MB of keys) in 8-slot buckets
 constexpr uint64_t kHotSlots = 1ull << kHotLog2;
 constexpr int kBucket = 8;
 
@@ -1326,9 +1329,13 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // layout or at i in the dense one (cap == 0).  Its kept records go to
 // kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
 // voff[c0], the range pass 0's scatter reads back.
-// the dedup bitmap covers the first 2^19 hot slots (64 KiB of LDS): two
-// workgroups per CU; with a larger hot level the rest is not deduplicated
-constexpr uint64_t kDedupSlots = kHotSlots < (1ull << 19) ? kHotSlots : (1ull << 19);
+// the dedup bitmap covers the first 2^II_DEDUP_LOG2 hot slots (1 bit each in
+// LDS); hot words beyond it are not deduplicated here (measured: covering
+// only half of a 2^20-slot hot level doubled the sort time)
+#ifndef II_DEDUP_LOG2
+#define II_DEDUP_LOG2 20  // the whole hot level: a 128 KiB bitmap, one 1024-thread workgroup per CU
+#endif
+constexpr uint64_t kDedupSlots = kHotSlots < (1ull << II_DEDUP_LOG2) ? kHotSlots : (1ull << II_DEDUP_LOG2);
 constexpr uint32_t kDedupWords = (uint32_t)(kDedupSlots / 32);
 #ifndef II_S0_DEFER
 #define II_S0_DEFER 0  // 1: a tile's kept records are stored one tile later (gathers overlap the next loads)
@@ -1337,17 +1344,17 @@ constexpr uint32_t kDedupWords = (uint32_t)(kDedupSlots / 32);
 #define II_S0_TTS 0
 #endif
 #ifndef II_S0_NT
-#define II_S0_NT 512
+#define II_S0_NT 1024
 #endif
 #ifndef II_S0_IT
-#define II_S0_IT 16
+#define II_S0_IT 8
 #endif
-constexpr int kCBlock = II_S0_NT;               // 8 waves share one 64 KiB dedup bitmap
+constexpr int kCBlock = II_S0_NT;               // 16 waves share one 128 KiB dedup bitmap
 constexpr int kS0Items = II_S0_IT;              // records per thread per tile
 constexpr int kCWaves = kCBlock / 64;
 constexpr int kCTile = kS0Items * kCBlock;    // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
-// LDS: 8 KiB counts + 64 KiB bitmap + 4 KiB offsets, so two workgroups fit a CU
+// LDS: 16 KiB counts + 128 KiB bitmap + 4 KiB offsets: one workgroup (16 waves) per CU
 
 template <bool kWid>
 __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
