@@ -18,6 +18,10 @@
 #include "ii_kernels.h"
 #include "ii_partial.h"
 
+#ifndef II_LV_BLOCKS
+#define II_LV_BLOCKS 8192  // grid cap of k_long_verify (grid-stride loop)
+#endif
+
 using namespace ii;
 
 namespace {
@@ -544,7 +548,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         }
         c->nlong = cnt[C_LONG];
         if (c->nlong) {
-            uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(c->nlong));
+            uint32_t g = (uint32_t)std::min<uint64_t>(II_LV_BLOCKS, grid_for(c->nlong));
             k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong,
                                                  P_<uint64_t>(c->trep), counters);
             HIPCK(hipGetLastError());

@@ -257,3 +257,24 @@ def test_logical_shards_balanced_letters(case, G):
     # histogram-balanced owners: same output, other ownership
     text, off, ids, expected = case_arrays(case)
     assert_same(shard_and_merge(text, off, G, balanced=True), expected, "%s G=%d balanced" % (case, G))
+
+
+def test_large_vocab_vs_oracle_both_key_modes():
+    # V ~ 2.2M distinct words (> 2^21): lexids need 22 bits, many words overflow
+    # the hot level, so the word-id keys mix hot slots and big-table ranks;
+    # the same corpus through lexid keys (the exchange path's sort) as well
+    t, off = ii_ctypes.zipf_corpus(200_000_000, 500, 5_000_000, 17, threads=8)
+    ids = list(range(500))
+    exp = oracle_index(t, off, ids)
+    ix = ii_ctypes.Index(0)
+    try:
+        for keys in ["wid", "lexid"]:
+            os.environ["II_SORT_KEYS"] = keys
+            ix.map_host(t, off.tolist(), ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, "vocab 5e6, %s keys" % keys)
+        st = ix.stats()
+        assert st.words > (1 << 21)
+    finally:
+        os.environ.pop("II_SORT_KEYS", None)
+        ix.close()
