@@ -159,7 +159,8 @@ int ii_reduce_local(ii_ctx *ctx);
  *   ii_reduce       -> orders and formats the owner's letters
  * Segment layout (little-endian, 8-byte aligned):
  *   u64 header[8] = {magic "IXIISEG1", nwords, npairs, arena_bytes,
- *                    letter_lo, letter_hi, 0, 0}
+ *                    letter_lo, letter_hi, 1 + smallest id0, 1 + largest id0}
+ *                   (the exporter's file ids; 0, 0 = unknown)
  *   u64 pairs[npairs] = (word index in segment) << 32 | id0
  *   u8  arena[arena_bytes rounded up to 8] = words in lexicographic order,
  *                    each followed by ' '

@@ -1152,7 +1152,9 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
         uint8_t* seg = (uint8_t*)d_send + send_off[r];
         uint64_t* pairs = (uint64_t*)(seg + 64);
         uint8_t* arena = seg + 64 + 8 * np;
-        k_export_header<<<1, 64, 0, c->st>>>((uint64_t*)seg, nw, np, ab, lo, hi);
+        const uint64_t id_lo1 = c->h_fid.empty() ? 0 : 1ull + c->h_fid.front();
+        const uint64_t id_hi1 = c->h_fid.empty() ? 0 : 1ull + c->h_fid.back();
+        k_export_header<<<1, 64, 0, c->st>>>((uint64_t*)seg, nw, np, ab, lo, hi, id_lo1, id_hi1);
         if (np)
             k_export_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
                 P_<uint64_t>(c->uniq), a[1], b[1], (uint32_t)a[0], pairs);
@@ -1229,7 +1231,20 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // (lexid, id0) order: LSD over the id bits, then the word bits
     int p1 = 0, p2 = 0;
     c->n_sc = 0;
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false, &p1));
+    // Every source's pairs arrive sorted by (word, id0) (K3 order; local and
+    // global lexicographic ids agree in order).  When the sources' id ranges
+    // ascend without overlap (ranks owning contiguous file ranges), a stable
+    // sort by word alone leaves (word, id0) order: the id pass is skipped.
+    bool ordered = true;
+    uint64_t prev_hi1 = 0;
+    for (int s = 0; s < nparts && ordered; s++) {
+        if (hdr[8 * s + 2] == 0) continue;
+        const uint64_t lo1 = hdr[8 * s + 6], hi1 = hdr[8 * s + 7];
+        if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
+        prev_hi1 = hi1;
+    }
+    if (!ordered || getenv("II_IMPORT_ID_SORT"))
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false, &p1));
     CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;

@@ -1842,10 +1842,14 @@ __global__ __launch_bounds__(kBlock) void k_export_pairs(const uint64_t* __restr
     }
 }
 
+// h[6], h[7] = 1 + the smallest / largest id0 of the exporting context's
+// files (0 = unknown): lets the owner skip its id sort when the sources' id
+// ranges ascend without overlap (ii_import)
 __global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint64_t npairs, uint64_t arena, uint64_t llo,
-                                uint64_t lhi) {
+                                uint64_t lhi, uint64_t id_lo1, uint64_t id_hi1) {
     if (threadIdx.x == 0) {
-        h[0] = kSegMagic; h[1] = nwords; h[2] = npairs; h[3] = arena; h[4] = llo; h[5] = lhi; h[6] = 0; h[7] = 0;
+        h[0] = kSegMagic; h[1] = nwords; h[2] = npairs; h[3] = arena; h[4] = llo; h[5] = lhi; h[6] = id_lo1;
+        h[7] = id_hi1;
     }
 }
 

@@ -202,7 +202,7 @@ def test_record_layouts_vs_oracle():
 
 
 # ---------------------------------------------------------------- multi-GPU exchange logic
-def shard_and_merge(text, off, G, id_bound=None, balanced=False):
+def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False):
     """G logical shards on one device: files split by the reference's size
     heuristic (ii_partition), each shard mapped in its own context, letter
     ranges exchanged (ii_export / ii_import) and formatted by their owner."""
@@ -210,6 +210,10 @@ def shard_and_merge(text, off, G, id_bound=None, balanced=False):
     n = len(off) - 1
     sizes = [off[i + 1] - off[i] for i in range(n)]
     order, sb, se = ii_ctypes.partition(sizes, G)
+    if contiguous:  # rank g owns files [g*n/G, (g+1)*n/G) (the bench's layout): ordered id ranges
+        order = list(range(n))
+        sb = [g * n // G for g in range(G)]
+        se = [(g + 1) * n // G for g in range(G)]
     idxs = []
     for g in range(G):
         fids = sorted(order[sb[g]:se[g]])
@@ -245,11 +249,22 @@ def test_logical_shards_match_reference(case, G):
     assert_same(shard_and_merge(text, off, G), expected, "%s G=%d" % (case, G))
 
 
+@pytest.mark.parametrize("case,G", [("config2", 3), ("zipf_small", 8), ("edge", 4), ("tiny360", 5)])
+def test_logical_shards_contiguous_ids(case, G):
+    # contiguous id ranges per shard: the owners skip their id sort (ii_import)
+    text, off, ids, expected = case_arrays(case)
+    assert_same(shard_and_merge(text, off, G, contiguous=True), expected, "%s G=%d contiguous" % (case, G))
+    assert_same(shard_and_merge(text, off, G, contiguous=True, balanced=True), expected,
+                "%s G=%d contiguous balanced" % (case, G))
+
+
 def test_logical_shards_zipf_vs_oracle():
     t, off = ii_ctypes.zipf_corpus(24_000_000, 300, 200_000, 33, threads=8)
     off = off.tolist()
     text = t.tobytes()
-    assert_same(shard_and_merge(text, off, 4), oracle_index(text, off, list(range(300))), "zipf G=4")
+    exp = oracle_index(text, off, list(range(300)))
+    assert_same(shard_and_merge(text, off, 4), exp, "zipf G=4")
+    assert_same(shard_and_merge(text, off, 4, contiguous=True), exp, "zipf G=4 contiguous")
 
 
 @pytest.mark.parametrize("case,G", [("config2", 3), ("zipf_small", 8), ("edge", 4)])
