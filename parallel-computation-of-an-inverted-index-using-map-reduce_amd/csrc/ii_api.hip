@@ -62,6 +62,7 @@ struct ii_ctx {
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
     DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
@@ -396,7 +397,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
-                   &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w};
+                   &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -1243,9 +1244,39 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
         prev_hi1 = hi1;
     }
-    if (!ordered || getenv("II_IMPORT_ID_SORT"))
-        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false, &p1));
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
+    if (ordered && !getenv("II_IMPORT_ID_SORT")) {
+        // merge the sorted segments by (word, source) runs: k_merge_runs / k_merge_scatter
+        const uint64_t nk = c->V * (uint64_t)nparts;
+        CK(grow(c->mstart, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
+        CK(grow(c->mend, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
+        uint64_t* ms = P_<uint64_t>(c->mstart);
+        uint64_t* me = P_<uint64_t>(c->mend);
+        HIPCK(hipMemsetAsync(me, 0, sizeof(uint64_t) * nk, c->st));
+        uint64_t pb = 0;
+        for (int s = 0; s < nparts; s++) {
+            const uint64_t np = hdr[8 * s + 2];
+            if (np)
+                k_merge_runs<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
+                    r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me);
+            pb += np;
+        }
+        CK(run_scan(c, OpMergeRuns{ms, me}, nk, nullptr));
+        pb = 0;
+        for (int s = 0; s < nparts; s++) {
+            const uint64_t np = hdr[8 * s + 2];
+            if (np)
+                k_merge_scatter<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
+                    r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me, r2);
+            pb += np;
+        }
+        HIPCK(hipGetLastError());
+        std::swap(r, r2);
+    } else {
+        if (!ordered || getenv("II_IMPORT_ID_SORT"))
+            CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false,
+                        &p1));
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
+    }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
     CK(run_unique(c, r, NP));

@@ -1865,4 +1865,37 @@ __global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restr
     }
 }
 
+// Owner-side merge of the received segments when their id ranges ascend
+// (ii_import): every segment is sorted by (lexid, id0), so the merged order
+// (lexid, source) is (lexid, id0).  Per (word w, source g): the run of the
+// word's pairs in segment g -> its place in the merged array (one scan over
+// V x G run lengths), then one scatter of coalesced runs instead of three
+// radix passes.
+__global__ __launch_bounds__(kBlock) void k_merge_runs(const uint64_t* __restrict__ r, uint64_t pb, uint64_t np,
+                                                       uint32_t G, uint32_t g, uint64_t* __restrict__ rstart,
+                                                       uint64_t* __restrict__ rend) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t w = (uint32_t)(r[pb + i] >> 32);
+        const uint64_t k = (uint64_t)w * G + g;
+        if (i == 0 || (uint32_t)(r[pb + i - 1] >> 32) != w) rstart[k] = pb + i;
+        if (i + 1 == np || (uint32_t)(r[pb + i + 1] >> 32) != w) rend[k] = pb + i + 1;
+    }
+}
+// run lengths (rend = 0: no run) -> exclusive offsets, in place in rend
+struct OpMergeRuns {
+    const uint64_t* rstart;
+    uint64_t* rend;
+    __device__ uint64_t value(uint64_t i) const { return rend[i] ? rend[i] - rstart[i] : 0; }
+    __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { rend[i] = ex; }
+};
+__global__ __launch_bounds__(kBlock) void k_merge_scatter(const uint64_t* __restrict__ r, uint64_t pb, uint64_t np,
+                                                          uint32_t G, uint32_t g, const uint64_t* __restrict__ rstart,
+                                                          const uint64_t* __restrict__ roff, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t v = r[pb + i];
+        const uint64_t k = (uint64_t)(uint32_t)(v >> 32) * G + g;
+        out[roff[k] + (pb + i - rstart[k])] = v;
+    }
+}
+
 }  // namespace ii

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Phase timing of the N > 1 path on ONE GPU (timing experiment, not product
+code): G logical shards of a Zipf corpus, each mapped in its own context on
+cuda:0 (rank-contiguous files, as bench.py lays them out), then the same
+steps ii_dist.exchange_and_reduce runs per rank — local reduce, plan +
+export, the exchange (device copies here; RCCL all-to-allv on a node),
+import, order + format — each timed across all G contexts.
+
+    python tools/exchange_timing.py [bytes_per_shard] [G] [steps]
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "bindings"))
+
+import torch  # noqa: E402
+
+import ii_ctypes  # noqa: E402
+import ii_dist  # noqa: E402
+
+
+def main():
+    nb = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(2e9)
+    G = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    files = 2000
+    texts = []
+    for g in range(G):
+        t, off = ii_ctypes.zipf_corpus(nb, files, 1_000_000, 3 + 1000 * g, threads=16)
+        d = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+        d[:nb].copy_(torch.from_numpy(t))
+        texts.append((d, off[:-1].tolist(), list(range(g * files, (g + 1) * files))))
+    torch.cuda.synchronize()
+    idxs = [ii_ctypes.Index(0) for _ in range(G)]
+    res = []
+    for it in range(steps + 1):
+        ph = {}
+
+        def lap(name, t0):
+            torch.cuda.synchronize()
+            ph[name] = ph.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
+
+        for g, ix in enumerate(idxs):
+            t0 = time.perf_counter()
+            d, fs, ids = texts[g]
+            ix.map_device(d.data_ptr(), nb, fs, ids)
+            lap("map", t0)
+            t0 = time.perf_counter()
+            ix.reduce_local()
+            lap("reduce_local", t0)
+        t0 = time.perf_counter()
+        lo, hi = ii_dist.owner_ranges([ix.letter_load() for ix in idxs], G)
+        sends = []
+        for ix in idxs:
+            sizes = ix.export_plan_ranges(lo, hi)
+            off, total = ii_dist.prefix(sizes)
+            buf = torch.empty(max(total, 8), dtype=torch.uint8, device="cuda")
+            ix.export(G, buf.data_ptr(), off)
+            sends.append((buf, sizes, off))
+        lap("plan_export", t0)
+        recvs = []
+        t0 = time.perf_counter()
+        for dst in range(G):
+            parts = [s[0][s[2][dst]:s[2][dst] + s[1][dst]] for s in sends]
+            recv_sizes = [s[1][dst] for s in sends]
+            recvs.append((torch.cat(parts) if sum(recv_sizes) else torch.empty(8, dtype=torch.uint8, device="cuda"),
+                          recv_sizes))
+        lap("exchange_copies", t0)
+        for dst, ix in enumerate(idxs):
+            t0 = time.perf_counter()
+            recv, rs = recvs[dst]
+            ix.import_(G, recv.data_ptr(), ii_dist.prefix(rs)[0], G * files)
+            lap("import", t0)
+            t0 = time.perf_counter()
+            ix.reduce(copy_text=False)
+            lap("order_format", t0)
+        ph["exchange_bytes"] = sum(sum(s[1]) for s in sends)
+        if it:
+            res.append(ph)
+    avg = {k: round(sum(r[k] for r in res) / len(res), 2) for k in res[0]}
+    avg["per_shard_ms"] = {k: round(v / G, 2) for k, v in avg.items() if k != "exchange_bytes"}
+    print(json.dumps({"G": G, "bytes_per_shard": nb, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
+                      "phases_ms_all_shards": avg}))
+    for ix in idxs:
+        ix.close()
+
+
+if __name__ == "__main__":
+    main()
