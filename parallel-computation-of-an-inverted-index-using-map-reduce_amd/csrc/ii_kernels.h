@@ -1551,7 +1551,9 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
 // "id0+1" takes its digits + 1 bytes (the following ' ' or ']',
 // main.c:228-234).  One reduce-then-scan yields both prefixes: uniq[u] = the
 // pair, P[u] = byte offset of its posting (P[p] - P[post_start[w]] is the
-// offset inside word w's list) and post_start[lexid] = the word's first pair.
+// offset inside word w's list; written only at word starts and u % 64 == 0,
+// the entries k_fmt_words / k_fmt_posts read) and post_start[lexid] = the
+// word's first pair.
 constexpr int kUniqItems = 4;                        // records per thread per tile
 constexpr int kUniqTile = kUniqItems * kBlock;       // item q of thread t: tile base + q * kBlock + t (coalesced)
 static_assert(kUniqItems * 16 <= 64, "per-item prefixes travel as 16-bit fields of one u64");
@@ -1662,9 +1664,12 @@ __global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restric
                 const uint64_t u = rc + ((ec >> (16 * q)) & 0xFFFFull);
                 const uint32_t key = (uint32_t)(r[q] >> 32);
                 uniq[u] = r[q];
-                P[u] = rb + ((eb >> (16 * q)) & 0xFFFFull);
                 const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
-                if (i == 0 || key != (uint32_t)(pv[q] >> 32)) {
+                const bool wstart = i == 0 || key != (uint32_t)(pv[q] >> 32);
+                // P is read at word starts (k_fmt_words, OpLineOff) and at the
+                // first posting of every 64 (k_fmt_posts) only
+                if (wstart || (u & 63u) == 0) P[u] = rb + ((eb >> (16 * q)) & 0xFFFFull);
+                if (wstart) {
                     post_start[key] = u;
                     if (i > 0) post_end[(uint32_t)(pv[q] >> 32)] = u;
                 }
@@ -1758,31 +1763,81 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
     out[o + len + 3 + (P[post_end[j]] - P[post_start[j]]) - 1] = '\n';
 }
 
-// uniq keys are wids or lexids, fbase is indexed the same way (k_fmt_words)
+// uniq keys are wids or lexids, fbase is indexed the same way (k_fmt_words).
+// A wave formats kFmtItems groups of 64 consecutive postings per iteration,
+// with every group's loads (pairs, then the fbase gathers) issued before any
+// digits are written: one dependent load chain per group left the pass
+// latency-bound.  A group reads the posting byte offset of its first posting
+// only (P is written at multiples of 64 and at word starts, k_uniq_apply) and
+// places the rest by a wave scan of their byte counts, so the pass reads
+// 8 bytes per posting instead of 16.
+#ifndef II_FMT_ITEMS
+#define II_FMT_ITEMS 4
+#endif
+constexpr int kFmtItems = II_FMT_ITEMS;
 __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
                                                       const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
                                                       uint8_t* __restrict__ out) {
-    for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < U; p += (uint64_t)gridDim.x * kBlock) {
-        uint64_t r = uniq[p];
-        uint32_t w = (uint32_t)(r >> 32);
-        const uint64_t id = (r & 0xFFFFFFFFull) + 1;
-        const uint64_t o = fbase[w] + P[p];
-        const uint32_t nd = id_digits(id);
-        if (id <= 0xFFFFFFFFull) {
-            uint32_t v = (uint32_t)id;
-            for (int i = (int)nd - 1; i >= 0; i--) {
-                out[o + i] = (uint8_t)('0' + v % 10u);
-                v /= 10u;
-            }
-        } else {
-            uint64_t v = id;
-            for (int i = (int)nd - 1; i >= 0; i--) {
-                out[o + i] = (uint8_t)('0' + v % 10u);
-                v /= 10u;
-            }
+    constexpr uint64_t kSpan = 64ull * kFmtItems;  // postings of one wave per iteration
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t g0 = ((uint64_t)blockIdx.x * kWaves + (uint64_t)wave_id()) * kSpan; g0 < U; g0 += nwaves * kSpan) {
+        uint64_t r[kFmtItems], pb[kFmtItems], fb[kFmtItems];
+        uint32_t wn[kFmtItems];
+#pragma unroll
+        for (int k = 0; k < kFmtItems; k++) {
+            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
+            r[k] = p < U ? uniq[p] : 0ull;
+            pb[k] = g0 + (uint64_t)k * 64 < U ? P[g0 + (uint64_t)k * 64] : 0ull;
         }
-        // last posting of the word: the next pair belongs to another word (runs are contiguous)
-        out[o + nd] = (p + 1 == U || (uint32_t)(uniq[p + 1] >> 32) != w) ? ']' : ' ';
+        // word of the posting after each group's lane 63 (the next group's lane 0)
+        const uint64_t pn = g0 + kSpan;
+        const uint32_t wtail = (lane_id() == 63 && pn < U) ? (uint32_t)(uniq[pn] >> 32) : 0u;
+#pragma unroll
+        for (int k = 0; k < kFmtItems; k++) {
+            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
+            fb[k] = p < U ? fbase[(uint32_t)(r[k] >> 32)] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kFmtItems; k++) {
+            const uint32_t w = (uint32_t)(r[k] >> 32);
+            uint32_t d = __shfl_down(w, 1, 64);
+            const uint32_t first_next = k + 1 < kFmtItems ? __shfl((uint32_t)(r[k + 1 < kFmtItems ? k + 1 : k] >> 32), 0, 64)
+                                                          : wtail;
+            wn[k] = lane_id() == 63 ? first_next : d;
+        }
+#pragma unroll
+        for (int k = 0; k < kFmtItems; k++) {
+            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
+            const bool live = p < U;
+            const uint32_t w = (uint32_t)(r[k] >> 32);
+            const uint64_t id = (r[k] & 0xFFFFFFFFull) + 1;
+            const uint32_t nd = id_digits(id);
+            const uint32_t len = live ? nd + 1u : 0u;
+            uint32_t inc = len;  // inclusive wave scan (64 postings x <= 11 bytes)
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o, 64);
+                if (lane_id() >= o) inc += t;
+            }
+            if (!live) continue;
+            // last posting of the word: the next pair belongs to another word (runs are contiguous)
+            const bool last = p + 1 == U || wn[k] != w;
+            const uint64_t o = fb[k] + pb[k] + (inc - len);
+            if (id <= 0xFFFFFFFFull) {
+                uint32_t v = (uint32_t)id;
+                for (int i = (int)nd - 1; i >= 0; i--) {
+                    out[o + i] = (uint8_t)('0' + v % 10u);
+                    v /= 10u;
+                }
+            } else {  // id0 = 2^32 - 1
+                uint64_t v = id;
+                for (int i = (int)nd - 1; i >= 0; i--) {
+                    out[o + i] = (uint8_t)('0' + v % 10u);
+                    v /= 10u;
+                }
+            }
+            out[o + nd] = last ? ']' : ' ';
+        }
     }
 }
 
