@@ -135,6 +135,44 @@ def test_noncontiguous_ids(idx):
     assert_same(idx.letters(), oracle_index(text, off, ids), "ids")
 
 
+def long_variant_corpus(seed, nfiles=60, per_file=3000):
+    """Long words (13-120 letters) written many ways: case changes, digits,
+    punctuation, high bytes and NULs inside, so that most occurrences differ
+    in their raw bytes from the word's representative and k_long_verify walks
+    them letter by letter (across several 16-byte blocks)."""
+    rng = random.Random(seed)
+    base = [bytes(rng.choice(LETTERS.encode()) for _ in range(rng.choice([13, 14, 17, 29, 31, 33, 64, 120])))
+            for _ in range(150)]
+    # words that agree on a long raw prefix and differ late
+    base += [b[:-1] + bytes([(b[-1] - 97 + 1) % 26 + 97]) for b in base[:40]]
+    other = b"0123456789.,'-_\x80\xc3\xa9\xff\x1c"
+    text = bytearray()
+    off = [0]
+    for _ in range(nfiles):
+        f = bytearray()
+        for _ in range(per_file // 40):
+            t = bytearray(rng.choice(base))
+            for i in range(len(t)):
+                if rng.random() < 0.2:
+                    t[i] ^= 0x20
+            for _ in range(rng.choice([0, 0, 1, 3, 8])):
+                t.insert(rng.randint(0, len(t)), rng.choice(other))
+            f += t + rng.choice([b" ", b"\n", b"\t"])
+        text += f
+        off.append(len(text))
+    return bytes(text), off, list(range(nfiles))
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_long_word_variants_vs_oracle(idx, seed):
+    text, off, ids = long_variant_corpus(seed)
+    idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(text, off, ids), "long variants %d" % seed)
+    # every variant verified as its word: no (false) hash collision forced a re-map
+    assert idx.stats().retries == 0
+
+
 def test_table_regrow_and_reuse():
     os.environ["II_TABLE_LOG2"] = "10"  # 1024-slot big table: forces several regrows
     try:
