@@ -167,6 +167,9 @@ constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
 #ifndef II_SC_IT
 #define II_SC_IT 16  // keys per thread per tile of the token-sort scatter
 #endif
+#ifndef II_HIST_V2
+#define II_HIST_V2 1  // k_radix_hist reads two keys per 16-B load
+#endif
 #ifndef II_SC_PF
 #define II_SC_PF 0  // 1: the scatter issues the next tile's loads before ranking this one
 #endif
@@ -183,6 +186,29 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint32_t* mine = cnt[wave_id()];
     const uint64_t tofs = (uint64_t)wave_id() * 64 * kSortItems + lane_id();
+#if II_HIST_V2
+    // the histogram ignores order: 16-B loads (two keys per lane, 1 KiB per
+    // wave instruction); lo and the tile are even, so a pair is split only at hi
+    (void)tofs;
+    const uint64_t pofs = (uint64_t)wave_id() * 64 * kSortItems + 2 * (uint64_t)lane_id();
+    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
+        ulonglong2 raw[kSortItems / 2];
+#pragma unroll
+        for (int k = 0; k < kSortItems / 2; k++) {
+            const uint64_t idx = tb + pofs + (uint64_t)k * 128;
+            if (idx + 1 < hi) {
+                const uint4 v = ld_nt16(keys + idx);
+                raw[k] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32));
+            } else raw[k] = make_ulonglong2(idx < hi ? keys[idx] : 0ull, 0ull);
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems / 2; k++) {
+            const uint64_t idx = tb + pofs + (uint64_t)k * 128;
+            if (idx < hi) atomicAdd(&mine[(uint32_t)(raw[k].x >> shift) & dmask], 1u);
+            if (idx + 1 < hi) atomicAdd(&mine[(uint32_t)(raw[k].y >> shift) & dmask], 1u);
+        }
+    }
+#else
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
         uint64_t raw[kSortItems];
 #pragma unroll
@@ -194,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
         for (int k = 0; k < kSortItems; k++)
             if (tb + tofs + (uint64_t)k * 64 < hi) atomicAdd(&mine[(uint32_t)(raw[k] >> shift) & dmask], 1u);
     }
+#endif
     __syncthreads();
     for (int d = threadIdx.x; d < kRadix; d += kBlock) {
         uint32_t t = 0;
