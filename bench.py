@@ -1,26 +1,44 @@
 #!/usr/bin/env python3
 """Benchmark: indexed input GB/s of the MI355X inverted-index builder.
 
-Workload (BASELINE.json configs[2]): synthetic Zipf corpus,
-10 GB across 10^4 files, vocabulary 10^6, seed 3, one MI355X per rank.  A
-"step" is one full pass of the hot path over the corpus: tokenize (K1), word
+Workloads (BASELINE.json configs):
+  config3       synthetic Zipf corpus, 10 GB across 10^4 files, vocabulary 10^6,
+                seed 3 — configs[2] on one MI355X; configs[3] ("the same corpus
+                sharded over 2/4/8") for N > 1
+  config5share  configs[4]'s per-GPU share: 12.5 GB across 1.25*10^5 files,
+                vocabulary 10^7, seed 5, one MI355X
+A "step" is one full pass of the hot path over the corpus: tokenize (K1), word
 table + lexicographic ids, token sort (K2), unique pairs (K3), final order
 (K4) and the formatted a..z index text (K5), all device-resident — the text
 is already in HBM when the timed region starts; nothing is cached across
 steps (every step re-tokenizes and rebuilds the index from scratch).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config3|config5share]
+                    [--scaling strong|weak]
 
-N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
-indexes its own 10 GB corpus (weak scaling): map + local reduce on its shard,
-one RCCL all-to-allv of letter ranges (ii_dist.exchange_and_reduce), and the
-owner's merge + order + format.  Rank 0 prints ONE JSON line.
+--gpus N > 1 without a torch.distributed environment starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child
+(before anything touches a GPU) and exits with its return code; one process
+per GPU, RCCL (backend "nccl") for the exchange.  Strong scaling (default):
+the files of the ONE corpus are assigned to ranks by the reference's size
+heuristic (ii_partition with M = N, main.c:300-323); each rank generates only
+its own files, maps and locally reduces them, one all-to-allv routes each
+letter range to its owner (histogram-balanced ranges, SURVEY §8 f4, or the
+reference's 26/N split, main.c:129-130), and the owners merge and format.
+--scaling weak: every rank indexes its own full-size corpus (seed + 1000*rank).
+
+After the timed loop (outside it) one more step copies the text out and every
+letter's sha256 is compared with tests/golden/bench_hashes.json (made by the
+oracle in the build container): "verified" in the JSON line.  Rank 0 prints
+ONE JSON line.
 """
 import argparse
-import ctypes
+import hashlib
 import json
 import os
 import shutil
+import socket
+import statistics
 import subprocess
 import sys
 import tempfile
@@ -31,6 +49,20 @@ PKG = os.path.join(REPO, "parallel-computation-of-an-inverted-index-using-map-re
 sys.path.insert(0, os.path.join(PKG, "bindings"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LETTERS = "abcdefghijklmnopqrstuvwxyz"
+
+WORKLOADS = {
+    "config3": dict(bytes=10_000_000_000, files=10_000, vocab=1_000_000, seed=3,
+                    label="zipf 10 GB x 10^4 files, vocab 10^6, seed 3"),
+    "config5share": dict(bytes=12_500_000_000, files=125_000, vocab=10_000_000, seed=5,
+                         label="zipf 12.5 GB x 1.25*10^5 files, vocab 10^7, seed 5 (configs[4] per-GPU share)"),
+}
+
+
+def log(msg):
+    """Progress on stderr (a long CPU-baseline lane is not a hang)."""
+    if os.environ.get("RANK", "0") == "0":
+        print("bench: %s" % msg, file=sys.stderr, flush=True)
 
 
 def parse():
@@ -38,35 +70,81 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--bytes", type=float, default=10e9, help="corpus bytes per rank")
-    p.add_argument("--files", type=int, default=10_000)
-    p.add_argument("--vocab", type=int, default=1_000_000)
-    p.add_argument("--seed", type=int, default=3)
-    p.add_argument("--cpu-sample-bytes", type=float, default=48e6)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="N > 1: shard one corpus over the ranks (strong) or one corpus per rank (weak)")
+    p.add_argument("--bytes", type=float, default=None, help="override the workload's corpus bytes")
+    p.add_argument("--files", type=int, default=None)
+    p.add_argument("--vocab", type=int, default=None)
+    p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--cpu-baseline", choices=["quick", "none"], default="quick")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-verify", action="store_true")
     p.add_argument("--gen-threads", type=int, default=16)
     p.add_argument("--io-bytes", type=float, default=2e9,
-                   help="bytes of the corpus written to files for the ii_map_files reader leg (0 = skip)")
+                   help="bytes of the corpus written to files for the file-reader and end-to-end legs (0 = skip)")
     p.add_argument("--letter-split", choices=["balanced", "reference"], default="balanced",
                    help="letter ownership of the N>1 exchange: histogram-balanced (SURVEY §8 f4) or the "
                         "reference's 26/N reducer split (main.c:129-130)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.no_cpu_baseline:
+        a.cpu_baseline = "none"
+    w = WORKLOADS[a.workload]
+    a.custom = any(v is not None for v in (a.bytes, a.files, a.vocab, a.seed))
+    a.bytes = int(a.bytes if a.bytes is not None else w["bytes"])
+    a.files = a.files if a.files is not None else w["files"]
+    a.vocab = a.vocab if a.vocab is not None else w["vocab"]
+    a.seed = a.seed if a.seed is not None else w["seed"]
+    return a
 
 
-def pmc_traffic():
-    """HBM bytes per launch by kernel from the committed rocprofv3 PMC summary
-    of this same bench command (profiles/*_pmc_traffic.json, newest round),
-    corrected as profiles/pmc_traffic.py documents; {} when absent."""
+def launch_ranks(a):
+    """N > 1 outside torch.distributed: one child launcher, N ranks, its rc."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def host_cores():
+    """CPU threads this job may use: the box exports OMP_NUM_THREADS as its
+    per-GPU CPU share (os.cpu_count() is the whole machine there)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
+def libii_sha16():
+    h = hashlib.sha256()
+    with open(os.path.join(PKG, "libii.so"), "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(build):
+    """HBM bytes per launch by kernel from the newest committed rocprofv3 PMC
+    summary (profiles/*_pmc_traffic.json, made by profiles/pmc_traffic.py from
+    this same bench command), only if it was measured on this very libii.so
+    build; ({}, reason) otherwise."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
     if not files:
-        return {}
+        return {}, "no PMC summary in profiles/"
     try:
         d = json.load(open(files[-1]))
-        return {k: round(v["traffic_bytes_per_launch"]) for k, v in d["kernels"].items()
-                if "traffic_bytes_per_launch" in v}
-    except Exception:
-        return {}
+    except Exception as e:  # noqa: BLE001
+        return {}, "unreadable %s: %s" % (os.path.basename(files[-1]), e)
+    if d.get("bench_line", {}).get("libii_sha16") != build:
+        return {}, "%s was measured on another libii.so build" % os.path.basename(files[-1])
+    return ({k: round(v["traffic_bytes_per_launch"]) for k, v in d["kernels"].items()
+             if "traffic_bytes_per_launch" in v}, os.path.basename(files[-1]))
 
 
 def safe_mappers(sizes, cores):
@@ -86,85 +164,132 @@ def safe_mappers(sizes, cores):
     return 1
 
 
-def cpu_baseline(text, off, sample_bytes):
-    """Time the reference itself (oracle/_ref/tema1, gcc -O2 build of
-    /root/reference/main.c) on the first files of the same corpus."""
+def write_files(text, off, nf, td):
     import numpy as np
+    names = []
+    for f in range(nf):
+        p = os.path.join(td, "f%06d.txt" % f)
+        np.asarray(text[int(off[f]):int(off[f + 1])]).tofile(p)
+        names.append(p)
+    with open(os.path.join(td, "list.txt"), "w") as fl:
+        fl.write("%d\n%s\n" % (nf, "\n".join(names)))
+    return names
+
+
+def cpu_baseline(a, text, off, runs=5):
+    """CPU baseline, bounded to about a minute:
+    the reference itself (oracle/_ref/tema1 = gcc -O2 main.c) on a
+    reference-feasible slice of the same generator — 360 files (its MAX_FILES,
+    main.c:8) of 25 KB — at M = cores / R = 26 and M = R = cores, median of
+    `runs` each; its as-shipped ASan build (Makefile:2) once for context; and
+    the multithreaded hash-based restatement (oracle ii_oracle_index_mt,
+    bit-exact) over the WHOLE corpus with `cores` threads.
+    value = the better reference median, in the metric's unit."""
+    import ii_ctypes
+    cores = host_cores()
     ref = os.path.join(REPO, "oracle", "_ref", "tema1")
-    nf = 0
-    while nf < min(360, len(off) - 1) and off[nf + 1] <= sample_bytes:  # reference MAX_FILES = 360
-        nf += 1
-    nf = max(nf, 1)
-    sb = int(off[nf])
-    cores = safe_mappers([int(off[f + 1] - off[f]) for f in range(nf)], min(16, os.cpu_count() or 1))
-    sample = "first %d files of the corpus (%.1f MB), M=%d mappers, R=26 reducers" % (nf, sb / 1e6, cores)
+    asan = os.path.join(REPO, "oracle", "_ref", "tema1_asan")
+    out = {"unit": "GB/s", "cores": cores, "host_cpus": os.cpu_count()}
+    sl_files, sl_bytes = 360, 360 * 25_000
+    st, so = ii_ctypes.zipf_corpus(sl_bytes, sl_files, a.vocab, a.seed + 77, threads=min(8, cores))
+    m_ok = safe_mappers([int(so[f + 1] - so[f]) for f in range(sl_files)], cores)
+    lanes = []
     if os.path.exists(ref):
         td = tempfile.mkdtemp(prefix="ii_cpu_")
         try:
-            names = []
-            for f in range(nf):
-                p = os.path.join(td, "f%05d.txt" % f)
-                np.asarray(text[int(off[f]):int(off[f + 1])]).tofile(p)
-                names.append(p)
-            with open(os.path.join(td, "list.txt"), "w") as fl:
-                fl.write("%d\n%s\n" % (nf, "\n".join(names)))
-            t0 = time.perf_counter()
-            subprocess.run([ref, str(cores), "26", "list.txt"], cwd=td, check=True, stdout=subprocess.DEVNULL,
-                           stderr=subprocess.DEVNULL, timeout=600)
-            dt = time.perf_counter() - t0
+            write_files(st, so, sl_files, td)
+
+            def timed(binary, M, R):
+                t0 = time.perf_counter()
+                subprocess.run([binary, str(M), str(R), "list.txt"], cwd=td, check=True, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL, timeout=600)
+                return time.perf_counter() - t0
+
+            for M, R in [(m_ok, 26), (m_ok, m_ok)]:
+                log("cpu baseline: reference M=%d R=%d x%d" % (M, R, runs))
+                ts = [timed(ref, M, R) for _ in range(runs)]
+                lanes.append({"binary": "tema1 (gcc -O2 main.c)", "M": M, "R": R, "runs": runs,
+                              "median_s": round(statistics.median(ts), 3), "all_s": [round(x, 3) for x in ts],
+                              "GBps": round(sl_bytes / statistics.median(ts) / 1e9, 6)})
+            if os.path.exists(asan):
+                log("cpu baseline: reference as shipped (ASan)")
+                t = timed(asan, m_ok, 26)
+                lanes.append({"binary": "tema1_asan (as shipped, -fsanitize=address -g)", "M": m_ok, "R": 26,
+                              "runs": 1, "median_s": round(t, 3), "GBps": round(sl_bytes / t / 1e9, 6)})
         finally:
             shutil.rmtree(td, ignore_errors=True)
-        return {"value": round(sb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "reference",
-                "sample": sample, "seconds": round(dt, 3)}
-    # reference binary absent: the oracle restatement, single thread
+        best = max(lanes[:2], key=lambda x: x["GBps"])
+        out.update({"value": best["GBps"], "kind": "reference", "M": best["M"], "R": best["R"],
+                    "sample": "reference binary on 360 files x 25 KB (%.1f MB) of the same generator (vocab %d); "
+                              "median of %d" % (sl_bytes / 1e6, a.vocab, runs), "reference_lanes": lanes})
+    # the bit-exact multithreaded restatement at full size
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_py import oracle_index
+    n = len(off) - 1
+    log("cpu baseline: multithreaded restatement over %.3g GB, %d threads" % (int(off[-1]) / 1e9, cores))
     t0 = time.perf_counter()
-    oracle_index(text[:sb], off[:nf + 1], list(range(nf)))
+    oracle_index(text, off, list(range(n)), threads=cores)
     dt = time.perf_counter() - t0
-    return {"value": round(sb / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": sample.replace("M=%d mappers, R=26 reducers" % cores, "oracle restatement, 1 thread"),
-            "seconds": round(dt, 3)}
+    full = {"kind": "port", "what": "oracle ii_oracle_index_mt (hash-based restatement, bit-exact), whole corpus",
+            "threads": cores, "bytes": int(off[-1]), "seconds": round(dt, 2), "GBps": round(int(off[-1]) / dt / 1e9, 4)}
+    out["restatement_full"] = full
+    if "value" not in out:  # no reference binary on this host: the restatement is the baseline
+        out.update({"value": full["GBps"], "kind": "port", "sample": full["what"]})
+    return out
 
 
-def io_leg(idx, text, off, io_bytes, threads=16):
-    """End-to-end file leg, reported beside `value`, never as
-    it: the first files of the corpus (<= io_bytes) are written to a scratch
-    directory, then ii_map_files reads them (pipelined pread into pinned
-    windows + async H2D, `threads` readers) and maps them.  Page cache warm
-    (the files were just written); best of 2."""
-    import numpy as np
+def io_legs(idx, text, off, io_bytes, cores):
+    """Beside `value`, never as it: the first files of the corpus (<= io_bytes)
+    are written to a scratch directory (page cache warm: just written), then
+      io  — ii_map_files reads them (pipelined pread into pinned windows +
+            async H2D, 16 readers, SURVEY §8 f2) and maps them; best of 2;
+      e2e — the drop-in CLI `ii_index M R list.txt` in a fresh process: list
+            file -> stat -> read + upload -> index -> a.txt..z.txt written to
+            disk, process start and HIP initialisation included."""
     nf = 0
     while nf < len(off) - 1 and off[nf + 1] <= io_bytes:
         nf += 1
     if nf == 0:
-        return None
+        return None, None
     td = tempfile.mkdtemp(prefix="ii_io_")
     try:
-        paths = []
-        for f in range(nf):
-            p = os.path.join(td, "f%05d.txt" % f)
-            np.asarray(text[int(off[f]):int(off[f + 1])]).tofile(p)
-            paths.append(p)
+        paths = write_files(text, off, nf, td)
         best = None
         for _ in range(2):
             t0 = time.perf_counter()
-            idx.map_files(paths, nthreads=threads)
+            idx.map_files(paths, nthreads=16)
             wall = time.perf_counter() - t0
             st = idx.stats()
             if best is None or wall < best[0]:
                 best = (wall, st.io_ms, st.io_bytes, st.ms_map)
+        wall, io_ms, io_b, map_ms = best
+        io = {"files": nf, "bytes": int(off[nf]), "threads": 16, "read_upload_ms": round(io_ms, 2),
+              "read_upload_GBps": round(io_b / (io_ms * 1e-3) / 1e9, 2) if io_ms > 0 else None,
+              "map_files_ms": round(wall * 1e3, 2), "map_files_GBps": round(int(off[nf]) / wall / 1e9, 2),
+              "k1_ms": round(map_ms, 2), "page_cache": "warm"}
+        M = min(16, cores)
+        runs = []
+        for _ in range(2):
+            wd = tempfile.mkdtemp(prefix="ii_e2e_", dir=td)
+            t0 = time.perf_counter()
+            r = subprocess.run([os.path.join(PKG, "ii_index"), str(M), "26", os.path.join(td, "list.txt")], cwd=wd,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+            runs.append(time.perf_counter() - t0)
+            if r.returncode != 0:
+                return io, {"error": r.stderr.decode()[-300:]}
+            out_b = sum(os.path.getsize(os.path.join(wd, l + ".txt")) for l in LETTERS)
+        e2e = {"what": "ii_index %d 26 list.txt (fresh process: HIP init, stat, read, index, write a..z.txt)" % M,
+               "files": nf, "bytes": int(off[nf]), "out_bytes": out_b, "wall_s": [round(x, 3) for x in runs],
+               "GBps": round(int(off[nf]) / min(runs) / 1e9, 3), "page_cache": "warm"}
+        return io, e2e
     finally:
         shutil.rmtree(td, ignore_errors=True)
-    wall, io_ms, io_b, map_ms = best
-    return {"files": nf, "bytes": int(off[nf]), "threads": threads, "read_upload_ms": round(io_ms, 2),
-            "read_upload_GBps": round(io_b / (io_ms * 1e-3) / 1e9, 2) if io_ms > 0 else None,
-            "map_files_ms": round(wall * 1e3, 2), "map_files_GBps": round(int(off[nf]) / wall / 1e9, 2),
-            "k1_ms": round(map_ms, 2), "page_cache": "warm"}
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -174,6 +299,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus == 1 and world > 1:
+        a.gpus = world
+    if a.gpus != world:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one process per GPU over RCCL (backend "nccl"); II_DIST_BACKEND=gloo rehearses the N>1 path on
@@ -187,30 +316,49 @@ def main():
             dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
+    strong = a.scaling == "strong" or world == 1
 
-    # ---- corpus: this rank's 10 GB (seed differs per rank), then to HBM
-    nbytes = int(a.bytes)
+    # ---- this rank's files, generated on the host, then to HBM
+    log("generating %s (%d rank(s), %s scaling)" % (a.workload, world, "strong" if strong else "weak"))
     t0 = time.perf_counter()
-    text, off = ii_ctypes.zipf_corpus(nbytes, a.files, a.vocab, a.seed + 1000 * rank, threads=a.gen_threads)
+    if strong:
+        layout = ii_ctypes.zipf_layout(a.bytes, a.files, a.seed)
+        if world > 1:  # the reference's size heuristic, one shard per GPU (main.c:300-323)
+            sizes = [int(x) for x in (layout[1:] - layout[:-1])]
+            order, sb, se = ii_ctypes.partition(sizes, world)
+            ids = sorted(order[sb[rank]:se[rank]])
+            text, off = ii_ctypes.zipf_shard(a.bytes, a.files, a.vocab, a.seed, ids, threads=a.gen_threads)
+        else:
+            ids = list(range(a.files))
+            text, off = ii_ctypes.zipf_corpus(a.bytes, a.files, a.vocab, a.seed, threads=a.gen_threads)
+        id_bound = a.files
+        total_bytes = a.bytes
+    else:
+        text, off = ii_ctypes.zipf_corpus(a.bytes, a.files, a.vocab, a.seed + 1000 * rank, threads=a.gen_threads)
+        ids = list(range(rank * a.files, (rank + 1) * a.files))  # rank r owns files [r*F, (r+1)*F)
+        id_bound = world * a.files
+        total_bytes = a.bytes * world
     gen_s = time.perf_counter() - t0
+    nbytes = int(off[-1])
     d_text = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
-    d_text[:nbytes].copy_(torch.from_numpy(text))
+    if nbytes:
+        d_text[:nbytes].copy_(torch.from_numpy(text[:nbytes]))
     torch.cuda.synchronize()
     file_start = off[:-1].tolist()
-    # global file IDs: rank r owns files [r*F, (r+1)*F)
-    ids = list(range(rank * a.files, (rank + 1) * a.files))
 
     idx = ii_ctypes.Index(local if world > 1 else 0)
+    owned = [(0, 26)]
 
-    id_bound = world * a.files
-
-    def step():
+    def step(copy_text=False):
         idx.map_device(d_text.data_ptr(), nbytes, file_start, ids)
         if world > 1:  # local reduce -> letter-range all-to-allv (RCCL) -> owner merge + format
-            ii_dist.exchange_and_reduce(idx, id_bound, balanced=a.letter_split == "balanced")
+            _, (lo, hi) = ii_dist.exchange_and_reduce(idx, id_bound, balanced=a.letter_split == "balanced",
+                                                      copy_text=copy_text)
+            owned[0] = (lo[rank], hi[rank])
         else:
-            idx.reduce(copy_text=False)
+            idx.reduce(copy_text=copy_text)
 
+    log("warmup %d + timed %d steps" % (a.warmup, a.steps))
     for _ in range(a.warmup):
         step()
     if world > 1:
@@ -234,26 +382,64 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt / a.steps * 1e3
-    total_bytes = nbytes * world
     value = total_bytes * a.steps / dt / 1e9
 
+    # ---- outside the timed region: the index itself, against the oracle's hashes
+    verified, verify_note, letter_sha = None, None, {}
+    if not a.no_verify:
+        log("verifying the index against the oracle's hashes")
+        step(copy_text=True)
+        lo, hi = owned[0]
+        mine = {LETTERS[l]: hashlib.sha256(idx.letter_text(l)).hexdigest() for l in range(lo, hi)}
+        if world > 1:
+            allh = [None] * world
+            dist.all_gather_object(allh, mine)
+            for h in allh:
+                letter_sha.update(h)
+        else:
+            letter_sha = mine
+        if rank == 0:
+            db = json.load(open(os.path.join(REPO, "tests", "golden", "bench_hashes.json")))["workloads"]
+            exp = db.get(a.workload)
+            if a.custom or not strong or exp is None:
+                verify_note = "no oracle hashes for this corpus (custom size or weak scaling)"
+            else:
+                bad = [l for l in LETTERS if letter_sha.get(l) != exp["letters"][l]["sha256"]]
+                verified = not bad and len(letter_sha) == 26
+                verify_note = "26 letters match the oracle (tests/golden/bench_hashes.json)" if verified else \
+                    "letters differ from the oracle: %s" % "".join(bad)
+
     if rank == 0:
+        build = libii_sha16()
         sc_ms = sum(scatter_ms) / len(scatter_ms)
         sc_achieved = st.scatter_bytes / (sc_ms * 1e-3) / 1e9 if sc_ms > 0 else 0.0
         em_ms = sum(emit_ms) / len(emit_ms)
         em_achieved = st.emit_bytes / (em_ms * 1e-3) / 1e9 if em_ms > 0 else 0.0
-        traffic = pmc_traffic()
-        # sort + segmented-reduce phase (K2 token sort + K3 unique), SURVEY §8d byte model:
-        # first pass 8 B per record read + 8 B per kept record written; each scatter pass
-        # 16 B per kept record; each later histogram pass 8 B per kept record; the unique
-        # scan reads the kept records twice and writes 16 B (pair + posting offset) per pair
-        T, Tk, U = st.tokens, st.sorted_records, st.pairs
+        traffic, traffic_src = pmc_traffic(build)
+        # sort + segmented-reduce phase (K2 token sort + K3 unique), two byte models:
+        #  survey: SURVEY §8d — first pass 8T + 8T_k, each radix pass 16 T_k, the unique
+        #          pass 8 T_k + 8 U + 16 V (what the algorithm must move)
+        #  impl:   what the kernels of this build move — plus one 8 T_k histogram read
+        #          per later pass, the unique count pass's second read of the records,
+        #          the posting offsets P (every word start and every 64th pair) and the
+        #          per-word start / end arrays
+        T, Tk, U, V = st.tokens, st.sorted_records, st.pairs, st.words
         sp = max(1, st.sort_passes)
-        ph_bytes = 8 * T + 8 * Tk + sp * 16 * Tk + (sp - 1) * 8 * Tk + 2 * 8 * Tk + 16 * U
+        survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
+        impl_b = 8 * T + 8 * Tk + sp * 16 * Tk + (sp - 1) * 8 * Tk + 2 * 8 * Tk + 8 * U + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
-        ph_achieved = ph_bytes / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
-        cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(text, off, a.cpu_sample_bytes)
-        io = io_leg(idx, text, off, a.io_bytes) if world == 1 and a.io_bytes > 0 else None
+        ph_gbs = survey_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
+        cpu = None
+        if a.cpu_baseline != "none" and world == 1:
+            cpu = cpu_baseline(a, text, off)
+        log("file reader and end-to-end legs")
+        io, e2e = io_legs(idx, text, off, a.io_bytes, host_cores()) if world == 1 and a.io_bytes > 0 else (None, None)
+        wl = WORKLOADS[a.workload]
+        workload = "%s: %s" % (a.workload, wl["label"] if not a.custom else "zipf %.4g GB x %d files, vocab %d, seed %d"
+                               % (a.bytes / 1e9, a.files, a.vocab, a.seed))
+        if a.workload == "config3":
+            workload += " (BASELINE configs[3]: sharded over %d GPUs by ii_partition)" % world if world > 1 and strong \
+                else " (BASELINE configs[2])" if world == 1 else " per rank (weak scaling)"
         line = {
             "metric": "indexed input GB/s (whole node) + % of HBM peak BW",
             "value": round(value, 3),
@@ -263,27 +449,34 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong and world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic Zipf corpus (tools/iigen.c, s~1, seed %d+1000*rank), device-resident" % a.seed,
-            "config": {"workload": "zipf %.3g GB x %d files/rank, vocab %d (BASELINE configs[2])" % (
-                nbytes / 1e9, a.files, a.vocab), "bytes_per_rank": nbytes, "files_per_rank": a.files,
-                "vocab": a.vocab, "parallelism": "shard-per-gpu x%d" % world,
-                "letter_split": a.letter_split if world > 1 else None},
+            "data": "synthetic Zipf corpus (tools/iigen.c, s~1), device-resident",
+            "verified": verified,
+            "verify": verify_note,
+            "config": {"workload": workload, "bytes": a.bytes if strong else a.bytes * world,
+                       "files": a.files if strong else a.files * world, "vocab": a.vocab, "seed": a.seed,
+                       "bytes_rank0": nbytes, "files_rank0": len(ids),
+                       "parallelism": "files by size over %d GPU(s) + letter-range all-to-allv" % world
+                       if world > 1 else "one GPU",
+                       "letter_split": a.letter_split if world > 1 else None},
             # dominant kernel: the tokenizer (K1b); algorithmic bytes = B + 8*T per launch
             "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
                          "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(em_achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic.get("ii::k_tok_emit<0>"),
+                         "traffic": traffic.get("ii::k_tok_emit<0>"), "traffic_source": traffic_src,
                          "bytes_per_launch": st.emit_bytes, "ms_per_launch": round(em_ms, 4)},
             "roofline_sort": {"bound": "hbm", "kernel": "k_radix_scatter (token sort passes)",
                               "achieved": round(sc_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(sc_achieved / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
             "roofline_sort_phase": {"bound": "hbm", "phase": "token sort + segmented unique (K2 + K3)",
-                                    "achieved": round(ph_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": round(ph_achieved / HBM_PEAK_GBS, 4), "bytes_per_step": ph_bytes,
+                                    "model": "SURVEY §8d", "achieved": round(ph_gbs, 1), "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 4),
+                                    "bytes_per_step": survey_b, "impl_bytes_per_step": impl_b,
+                                    "impl_frac": round(impl_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                    if ph_ms > 0 else 0.0,
                                     "ms_per_step": round(ph_ms, 4),
                                     "first_pass": {"kernel": "k_sort0_compact", "ms": round(st.sort0_ms, 4),
                                                    "bytes": st.sort0_bytes,
@@ -291,12 +484,15 @@ def main():
                                                    if st.sort0_ms > 0 else 0.0}},
             "cpu_baseline": cpu,
             "io": io,
+            "e2e": e2e,
             "phases_ms": {k: round(getattr(st, k), 3) for k in
                           ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total",
                            "emit_ms", "resolve_ms"]},
             "counts": {"tokens": st.tokens, "pairs": st.pairs, "words": st.words, "long_tokens": st.long_tokens,
                        "out_bytes": st.out_bytes, "sort_passes": st.sort_passes, "table_cap": st.table_cap,
                        "resolved_tokens": st.resolved_tokens, "sorted_records": st.sorted_records},
+            "output_letter_sha256": letter_sha if letter_sha else None,
+            "libii_sha16": build,
             "gen_seconds": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)

@@ -45,11 +45,14 @@ typedef struct ii_ctx ii_ctx;
 
 /* One input file of a shard.  Replaces FileInfo (main.c:14-18).  id0 is the
  * 0-based position in the list file (main.c:275) and is printed as id0+1
- * (main.c:116). */
+ * (main.c:116).  mapper is the reference mapper whose shard holds the file
+ * (ii_partition, main.c:300-323): only printed, in the missing-file message
+ * "Mapper <mapper>: Error opening file <path>" (main.c:98); 0 if unknown. */
 typedef struct {
     const char *path;
     uint64_t size;
     uint32_t id0;
+    int32_t mapper;
 } ii_file;
 
 /* Per-run counters (no reference equivalent; the reference only prints). */
@@ -104,8 +107,8 @@ const char *ii_strerror(int code);
  * would have written to partial_<letter>.txt.
  *
  * Files must be given in ascending id0 order.  Missing / unreadable files are
- * reported on stderr in the reference's wording (main.c:98) and contribute
- * nothing; they are not an error.  `nthreads` host reader threads (the
+ * reported once on stderr in the reference's wording (main.c:98, with
+ * ii_file.mapper) and contribute nothing; they are not an error.  `nthreads` host reader threads (the
  * reference's M, at most 16) read the files: files[f].size (the stat size)
  * fixes each file's place on the device, the threads pread 8 MiB windows
  * into pinned buffers and upload each with an async copy on their own stream

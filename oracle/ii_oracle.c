@@ -31,6 +31,7 @@
  * scan (main.c:172-173) — same result, O(T) instead of O(T*V).
  */
 #define _GNU_SOURCE
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -235,6 +236,142 @@ int ii_oracle_index(const unsigned char *text, const uint64_t *file_off, const u
 }
 
 void ii_oracle_free(void *p) { free(p); }
+
+/*
+ * Multithreaded form of ii_oracle_index (the CPU baseline of bench.py at full
+ * size, and the generator of tests/golden/bench_hashes.json).  Same result,
+ * same rules; the reference's two phases with `nthreads` workers each:
+ *   map    (mapper(), main.c:85-124): thread k tokenizes a contiguous run of
+ *          files (ascending IDs) into its own 26 per-letter dictionaries;
+ *   reduce (reducer(), main.c:126-242): letters are taken from a shared
+ *          counter; a letter's thread-local dictionaries are merged in thread
+ *          order — thread k's IDs all exceed thread k-1's, so appending keeps
+ *          every posting list ascending with no dedup across threads — then
+ *          ordered and formatted as in or_reduce_letter.
+ */
+typedef struct {
+    const unsigned char *text;
+    const uint64_t *file_off;
+    const uint32_t *file_id0;
+    uint32_t f_lo, f_hi;
+    or_dict dicts[OR_ALPHA];
+} or_map_job;
+
+static void *or_map_worker(void *p) {
+    or_map_job *j = p;
+    for (uint32_t f = j->f_lo; f < j->f_hi; f++)
+        or_map_bytes(j->dicts, j->text + j->file_off[f], j->file_off[f + 1] - j->file_off[f], j->file_id0[f] + 1);
+    return NULL;
+}
+
+/* Append src's postings of one word to dst (src's IDs all exceed dst's). */
+static void or_dict_merge_entry(or_dict *d, or_entry *src) {
+    if ((uint64_t)(d->n + 1) * 2 > d->mask + 1) or_dict_grow(d);
+    uint64_t s = src->hash & d->mask;
+    for (;;) {
+        uint32_t x = d->slot[s];
+        if (!x) break;
+        or_entry *e = &d->e[x - 1];
+        if (e->hash == src->hash && e->len == src->len && memcmp(e->word, src->word, src->len) == 0) {
+            if (e->n + src->n > e->cap) {
+                while (e->n + src->n > e->cap) e->cap *= 2;
+                e->ids = realloc(e->ids, e->cap * sizeof(uint32_t));
+                if (!e->ids) { fprintf(stderr, "oracle: out of memory\n"); exit(EXIT_FAILURE); }
+            }
+            memcpy(e->ids + e->n, src->ids, src->n * sizeof(uint32_t));
+            e->n += src->n;
+            free(src->ids);
+            free(src->word);
+            return;
+        }
+        s = (s + 1) & d->mask;
+    }
+    if (d->n == d->cap) {
+        d->cap = d->cap ? d->cap * 2 : 1024;
+        d->e = realloc(d->e, d->cap * sizeof(or_entry));
+        if (!d->e) { fprintf(stderr, "oracle: out of memory\n"); exit(EXIT_FAILURE); }
+    }
+    d->e[d->n] = *src; /* takes ownership of word and ids */
+    d->slot[s] = ++d->n;
+}
+
+typedef struct {
+    or_map_job *maps;
+    int nmaps;
+    char *parts[OR_ALPHA];
+    uint64_t lens[OR_ALPHA];
+    int next;
+    pthread_mutex_t mu;
+} or_reduce_job;
+
+static void *or_reduce_worker(void *p) {
+    or_reduce_job *j = p;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        int l = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (l >= OR_ALPHA) break;
+        or_dict acc;
+        memset(&acc, 0, sizeof(acc));
+        for (int k = 0; k < j->nmaps; k++) {
+            or_dict *src = &j->maps[k].dicts[l];
+            for (uint32_t i = 0; i < src->n; i++) or_dict_merge_entry(&acc, &src->e[i]);
+            free(src->e);
+            free(src->slot);
+            memset(src, 0, sizeof(*src));
+        }
+        j->parts[l] = or_reduce_letter(&acc, &j->lens[l]);
+        or_dict_free(&acc);
+    }
+    return NULL;
+}
+
+int ii_oracle_index_mt(const unsigned char *text, const uint64_t *file_off, const uint32_t *file_id0,
+                       uint32_t nfiles, int nthreads, char **out, uint64_t letter_off[OR_ALPHA + 1]) {
+    for (uint32_t f = 1; f < nfiles; f++)
+        if (file_id0[f] <= file_id0[f - 1]) return -1; /* IDs must ascend */
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    /* contiguous file runs of about equal bytes */
+    or_map_job *maps = calloc((size_t)nthreads, sizeof(or_map_job));
+    const uint64_t total = nfiles ? file_off[nfiles] - file_off[0] : 0;
+    uint32_t f = 0;
+    for (int k = 0; k < nthreads; k++) {
+        maps[k].text = text;
+        maps[k].file_off = file_off;
+        maps[k].file_id0 = file_id0;
+        maps[k].f_lo = f;
+        const uint64_t goal = nfiles ? file_off[0] + total * (uint64_t)(k + 1) / (uint64_t)nthreads : 0;
+        while (f < nfiles && (k == nthreads - 1 || file_off[f + 1] <= goal)) f++;
+        maps[k].f_hi = f;
+    }
+    pthread_t th[256];
+    for (int k = 0; k < nthreads; k++) pthread_create(&th[k], NULL, or_map_worker, &maps[k]);
+    for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    or_reduce_job rj;
+    memset(&rj, 0, sizeof(rj));
+    rj.maps = maps;
+    rj.nmaps = nthreads;
+    pthread_mutex_init(&rj.mu, NULL);
+    const int nr = nthreads < OR_ALPHA ? nthreads : OR_ALPHA;
+    for (int k = 0; k < nr; k++) pthread_create(&th[k], NULL, or_reduce_worker, &rj);
+    for (int k = 0; k < nr; k++) pthread_join(th[k], NULL);
+    pthread_mutex_destroy(&rj.mu);
+    free(maps);
+    uint64_t sum = 0;
+    for (int l = 0; l < OR_ALPHA; l++) sum += rj.lens[l];
+    char *buf = malloc(sum + 1);
+    uint64_t o = 0;
+    for (int l = 0; l < OR_ALPHA; l++) {
+        letter_off[l] = o;
+        memcpy(buf + o, rj.parts[l], rj.lens[l]);
+        o += rj.lens[l];
+        free(rj.parts[l]);
+    }
+    letter_off[OR_ALPHA] = o;
+    *out = buf;
+    return 0;
+}
 
 /* Partial files (main.c:113-118, format "%s %d\n" at main.c:116): one growing
  * buffer per letter. */

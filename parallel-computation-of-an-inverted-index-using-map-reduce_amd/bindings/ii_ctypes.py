@@ -49,7 +49,8 @@ class Stats(ctypes.Structure):
 
 
 class IIFile(ctypes.Structure):
-    _fields_ = [("path", ctypes.c_char_p), ("size", ctypes.c_uint64), ("id0", ctypes.c_uint32)]
+    _fields_ = [("path", ctypes.c_char_p), ("size", ctypes.c_uint64), ("id0", ctypes.c_uint32),
+                ("mapper", ctypes.c_int32)]
 
 
 _lib = None
@@ -159,9 +160,10 @@ class Index:
                                    len(file_id0), hist), "ii_map_device")
         return list(hist)
 
-    def map_files(self, paths, nthreads=4, id0=None, sizes=None):
+    def map_files(self, paths, nthreads=4, id0=None, sizes=None, mappers=None):
         """ii_map_files; `sizes` overrides the stat sizes (tests of the
-        reader's short-file padding and grown-file fallback)."""
+        reader's short-file padding and grown-file fallback); `mappers` the
+        mapper id printed for a missing file (main.c:98)."""
         files = (IIFile * max(1, len(paths)))()
         keep = []
         for i, p in enumerate(paths):
@@ -170,7 +172,7 @@ class Index:
             size = os.path.getsize(p) if os.path.exists(p) else 0
             if sizes is not None:
                 size = sizes[i]
-            files[i] = IIFile(b, size, i if id0 is None else id0[i])
+            files[i] = IIFile(b, size, i if id0 is None else id0[i], 0 if mappers is None else mappers[i])
         hist = (ctypes.c_uint64 * ALPHABET)()
         _check(lib().ii_map_files(self.h, files, len(paths), nthreads, hist), "ii_map_files")
         return list(hist)
@@ -293,3 +295,35 @@ def zipf_corpus(total_bytes, nfiles, vocab, seed, threads=8, out=None):
     if g.iigen_fill(ctypes.byref(p), ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(out.ctypes.data), threads) != 0:
         raise RuntimeError("iigen_fill failed")
     return out[:total_bytes], off
+
+
+def zipf_layout(total_bytes, nfiles, seed):
+    """File offsets (numpy u64[nfiles+1]) of the corpus zipf_corpus would make,
+    without making it (the sizes ii_partition shards by)."""
+    import numpy as np
+    p = GenParams(total_bytes, nfiles, 1, seed, 1.0)
+    off = np.zeros(nfiles + 1, dtype=np.uint64)
+    if genlib().iigen_layout(ctypes.byref(p), ctypes.c_void_p(off.ctypes.data)) != 0:
+        raise RuntimeError("iigen_layout failed")
+    return off
+
+
+def zipf_shard(total_bytes, nfiles, vocab, seed, files, threads=8, pad=16):
+    """Only the files `files` (indices, any order) of zipf_corpus(total_bytes,
+    nfiles, vocab, seed), back to back in that order — one GPU's shard.
+    Returns (numpy u8 text, numpy u64 offsets[len(files)+1]); the bytes of every
+    file equal its slice of the whole corpus."""
+    import numpy as np
+    p = GenParams(total_bytes, nfiles, vocab, seed, 1.0)
+    full = zipf_layout(total_bytes, nfiles, seed)
+    sel = np.ascontiguousarray(np.asarray(list(files), dtype=np.uint32))
+    sizes = (full[1:] - full[:-1])[sel.astype(np.int64)] if len(sel) else np.zeros(0, dtype=np.uint64)
+    n = int(sizes.sum())
+    out = np.empty(n + pad, dtype=np.uint8)
+    off = np.zeros(len(sel) + 1, dtype=np.uint64)
+    g = genlib()
+    if g.iigen_fill_files(ctypes.byref(p), ctypes.c_void_p(full.ctypes.data),
+                          ctypes.c_void_p(sel.ctypes.data if len(sel) else None), ctypes.c_uint32(len(sel)),
+                          ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(out.ctypes.data), threads) != 0:
+        raise RuntimeError("iigen_fill_files failed")
+    return out[:n], off

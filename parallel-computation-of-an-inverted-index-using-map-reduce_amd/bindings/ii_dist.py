@@ -79,6 +79,10 @@ def exchange_and_reduce(idx, id_bound, group=None, copy_text=False, balanced=Fal
     recv_off, _ = prefix(recv_sizes)
     if recv.numel() == 0:
         recv = torch.empty(8, dtype=torch.uint8, device="cuda")
+    # the collective (or gloo's host -> device copy) was queued on torch's
+    # current stream; libii reads recv on its own stream, so the bytes must
+    # have landed before ii_import starts
+    torch.cuda.current_stream().synchronize()
     idx.import_(world, recv.data_ptr(), recv_off, id_bound)
     idx.reduce(copy_text=copy_text)
     return recv_sizes, (lo, hi)

@@ -691,7 +691,7 @@ static void io_fill(IoJob* j, uint64_t lo, uint64_t hi, uint8_t* buf) {
             const int fd = open(j->files[f].path, O_RDONLY);
             const bool first = j->off[f] >= lo;
             if (fd < 0) {
-                if (first) fprintf(stderr, "Mapper %d: Error opening file %s\n", 0, j->files[f].path);
+                if (first) fprintf(stderr, "Mapper %d: Error opening file %s\n", j->files[f].mapper, j->files[f].path);
                 if (b > a) memset(buf + (a - lo), ' ', b - a);
             } else {
                 uint64_t done = 0;
@@ -761,6 +761,8 @@ static int io_setup(ii_ctx* c, int nt) {
 }
 
 // Whole-file reads, then one copy (files whose size was not known up front).
+// The pipelined pass that found a grown file has already reported the
+// missing ones (main.c:98), so this pass skips them quietly.
 struct ReadJob {
     const ii_file* files;
     uint32_t n;
@@ -776,10 +778,7 @@ void* read_worker(void* arg) {
         pthread_mutex_unlock(&j->mu);
         if (f >= j->n) break;
         FILE* fp = fopen(j->files[f].path, "rb");
-        if (!fp) {
-            fprintf(stderr, "Mapper %d: Error opening file %s\n", 0, j->files[f].path);  // main.c:98
-            continue;
-        }
+        if (!fp) continue;  // reported by io_fill
         std::vector<uint8_t>& d = (*j->data)[f];
         d.resize(j->files[f].size ? j->files[f].size + 1 : 4096);
         size_t len = 0, r;

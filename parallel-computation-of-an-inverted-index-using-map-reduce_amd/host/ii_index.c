@@ -99,7 +99,10 @@ int main(int argc, char **argv) {
     uint32_t *order = calloc((size_t)count + 1, sizeof(uint32_t));
     uint32_t *sb = calloc((size_t)M, sizeof(uint32_t)), *se = calloc((size_t)M, sizeof(uint32_t));
     ii_partition(sizes, (uint32_t)count, M, order, sb, se);
-    for (int m = 0; m < M; m++) printf("Mapper %d: Files %u to %u\n", m, sb[m], se[m]);
+    for (int m = 0; m < M; m++) {
+        printf("Mapper %d: Files %u to %u\n", m, sb[m], se[m]);
+        for (uint32_t i = sb[m]; i < se[m]; i++) files[order[i]].mapper = m; /* main.c:98 names it */
+    }
 
     ii_ctx *ctx = NULL;
     int rc = ii_open(&ctx, 0);

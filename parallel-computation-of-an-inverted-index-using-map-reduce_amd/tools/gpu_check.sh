@@ -3,13 +3,13 @@
 # rocprofv3 kernel statistics of the same bench command.  Every GPU step runs
 # under its own time limit and the steps are chained with &&, so the first
 # failure ends the session.
-#   tools/gpu_check.sh TAG [BENCH_BYTES] [STEPS] [SKIP_TESTS]
+#   tools/gpu_check.sh TAG [STEPS] [SKIP_TESTS] [TEST_SELECTION]
 # Results land in gpurun_out/TAG/.
 set -o pipefail
 TAG=${1:-run}
-BYTES=${2:-10e9}
-STEPS=${3:-5}
-SKIP_TESTS=${4:-0}
+STEPS=${2:-10}
+SKIP_TESTS=${3:-0}
+SEL=${4:-tests}
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 PKG="$ROOT/parallel-computation-of-an-inverted-index-using-map-reduce_amd"
 OUT="$ROOT/gpurun_out/$TAG"
@@ -20,7 +20,8 @@ export TMPDIR=/tmp
 run_tests() {
     [ "$SKIP_TESTS" = "1" ] && return 0
     echo "== tests"
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    # shellcheck disable=SC2086
+    timeout -k 10 900 python -u -m pytest $SEL -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1
     local rc=$?
     tail -3 "$OUT/pytest_gpu.log"
@@ -37,10 +38,10 @@ run_ablate() {
 
 run_tests && run_ablate && \
 echo "== bench" && \
-timeout -k 10 480 python bench.py --steps "$STEPS" --warmup 2 --bytes "$BYTES" > "$OUT/bench.log" 2>&1 && \
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 2 > "$OUT/bench.log" 2>&1 && \
 tail -1 "$OUT/bench.log" && \
 echo "== rocprof" && \
 timeout -k 10 480 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 1 --bytes "$BYTES" --no-cpu-baseline --io-bytes 0 > "$OUT/prof.log" 2>&1 && \
+    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify > "$OUT/prof.log" 2>&1 && \
 tail -1 "$OUT/prof.log" && \
 find "$OUT/prof" -name '*kernel_stats.csv' -exec head -16 {} \;

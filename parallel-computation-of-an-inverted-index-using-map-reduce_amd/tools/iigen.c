@@ -58,6 +58,9 @@ typedef struct {
     double logv;
     const uint64_t *file_off;
     uint8_t *out;
+    const uint32_t *sel;     /* iigen_fill_files: the files to make (NULL = all) */
+    const uint64_t *sel_off; /* their places in out */
+    uint32_t nwork;          /* files to make */
     uint32_t next_file;
     pthread_mutex_t mu;
 } gen_ctx;
@@ -161,12 +164,12 @@ static void *worker(void *arg) {
     gen_ctx *g = arg;
     for (;;) {
         pthread_mutex_lock(&g->mu);
-        uint32_t f = g->next_file;
-        uint32_t take = 1;
-        if (f < g->p->nfiles) g->next_file += take;
+        uint32_t k = g->next_file;
+        if (k < g->nwork) g->next_file++;
         pthread_mutex_unlock(&g->mu);
-        if (f >= g->p->nfiles) break;
-        gen_file(g, f, g->out + g->file_off[f], g->file_off[f + 1] - g->file_off[f]);
+        if (k >= g->nwork) break;
+        const uint32_t f = g->sel ? g->sel[k] : k;
+        gen_file(g, f, g->out + (g->sel ? g->sel_off[k] : g->file_off[f]), g->file_off[f + 1] - g->file_off[f]);
     }
     return NULL;
 }
@@ -200,11 +203,15 @@ int iigen_layout(const iigen_params *p, uint64_t *file_off) {
     return 0;
 }
 
-int iigen_fill(const iigen_params *p, const uint64_t *file_off, uint8_t *out, int nthreads) {
+static int fill_core(const iigen_params *p, const uint64_t *file_off, const uint32_t *sel, const uint64_t *sel_off,
+                     uint32_t nsel, uint8_t *out, int nthreads) {
     if (!p || !file_off || !out || p->vocab == 0) return -1;
     gen_ctx g;
     memset(&g, 0, sizeof(g));
     g.p = p;
+    g.sel = sel;
+    g.sel_off = sel_off;
+    g.nwork = sel ? nsel : p->nfiles;
     uint32_t acc = 0;
     for (int l = 0; l < 26; l++) { acc += kFreq[l]; g.cdf[l] = acc; }
     g.cdf_total = acc;
@@ -222,6 +229,27 @@ int iigen_fill(const iigen_params *p, const uint64_t *file_off, uint8_t *out, in
     free(g.words);
     free(g.woff);
     return 0;
+}
+
+int iigen_fill(const iigen_params *p, const uint64_t *file_off, uint8_t *out, int nthreads) {
+    return fill_core(p, file_off, NULL, NULL, 0, out, nthreads);
+}
+
+/* A subset of the corpus (a GPU's shard): files sel[0..nsel) (any order; each
+ * file's bytes are exactly those iigen_fill gives it, since every file has its
+ * own random stream) back to back in out, file sel[k] at out_off[k]
+ * (out_off[0] = 0, out_off[k + 1] = out_off[k] + its size; nsel + 1 entries
+ * written). */
+int iigen_fill_files(const iigen_params *p, const uint64_t *file_off, const uint32_t *sel, uint32_t nsel,
+                     uint64_t *out_off, uint8_t *out, int nthreads) {
+    if (!p || !file_off || (nsel && !sel) || !out_off) return -1;
+    out_off[0] = 0;
+    for (uint32_t k = 0; k < nsel; k++) {
+        if (sel[k] >= p->nfiles) return -1;
+        out_off[k + 1] = out_off[k] + (file_off[sel[k] + 1] - file_off[sel[k]]);
+    }
+    if (nsel == 0) return 0;
+    return fill_core(p, file_off, sel, out_off, nsel, out, nthreads);
 }
 
 #ifdef IIGEN_MAIN

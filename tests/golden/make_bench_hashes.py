@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Per-letter sha256 of the index of the benchmark corpora, made by the oracle
+(oracle/ii_oracle.c, pinned against the reference binary on every golden case)
+in the build container — TEST INFRASTRUCTURE ONLY.
+
+bench.py hashes its own device output after the timed loop and reports
+"verified": true only when every letter matches the entry written here;
+tests/test_gpu_bench_verify.py asserts the same at full size on the GPU box.
+
+    python tests/golden/make_bench_hashes.py [workload ...]
+
+Workloads (bench.py --workload):
+  config3        BASELINE configs[2]/[3]: 10 GB Zipf, 10^4 files, vocab 10^6, seed 3
+  config5share   configs[4]'s per-GPU share: 12.5 GB, 1.25*10^5 files, vocab 10^7, seed 5
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "parallel-computation-of-an-inverted-index-using-map-reduce_amd", "bindings"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+WORKLOADS = {
+    "config3": dict(total_bytes=10_000_000_000, nfiles=10_000, vocab=1_000_000, seed=3),
+    "config5share": dict(total_bytes=12_500_000_000, nfiles=125_000, vocab=10_000_000, seed=5),
+}
+OUT = os.path.join(HERE, "bench_hashes.json")
+
+
+def main(names):
+    import ii_ctypes
+    from oracle_py import oracle_index
+    db = json.load(open(OUT)) if os.path.exists(OUT) else {"workloads": {}}
+    for name in names:
+        p = WORKLOADS[name]
+        t0 = time.time()
+        text, off = ii_ctypes.zipf_corpus(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], threads=8)
+        corpus_sha = hashlib.sha256(memoryview(text)).hexdigest()
+        t1 = time.time()
+        res = oracle_index(text, off, list(range(p["nfiles"])))
+        t2 = time.time()
+        letters = {l: {"sha256": hashlib.sha256(v).hexdigest(), "bytes": len(v), "lines": v.count(b"\n")}
+                   for l, v in res.items()}
+        db["workloads"][name] = {"iigen": p, "corpus_sha256": corpus_sha, "letters": letters,
+                                 "out_bytes": sum(x["bytes"] for x in letters.values()),
+                                 "words": sum(x["lines"] for x in letters.values()),
+                                 "oracle_seconds": round(t2 - t1, 1), "gen_seconds": round(t1 - t0, 1)}
+        print(name, "words", db["workloads"][name]["words"], "out", db["workloads"][name]["out_bytes"],
+              "oracle %.1fs" % (t2 - t1), flush=True)
+        del text, res
+        json.dump(db, open(OUT, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(WORKLOADS))

@@ -14,6 +14,8 @@ def _load():
         _lib = ctypes.CDLL(_ORACLE)
         _lib.ii_oracle_index.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+        _lib.ii_oracle_index_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
         _lib.ii_oracle_free.argtypes = [ctypes.c_void_p]
         _lib.ii_oracle_partials.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                             ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
@@ -21,8 +23,9 @@ def _load():
     return _lib
 
 
-def oracle_index(text, file_off, file_id0):
-    """-> {letter: bytes} exactly as the reference would write a.txt..z.txt."""
+def oracle_index(text, file_off, file_id0, threads=1):
+    """-> {letter: bytes} exactly as the reference would write a.txt..z.txt.
+    threads > 1: the multithreaded restatement (ii_oracle_index_mt)."""
     import numpy as np
     L = _load()
     if hasattr(text, "ctypes"):
@@ -33,8 +36,12 @@ def oracle_index(text, file_off, file_id0):
     ids = np.ascontiguousarray(np.asarray(file_id0, dtype=np.uint32))
     out = ctypes.c_void_p()
     loff = (ctypes.c_uint64 * 27)()
-    rc = L.ii_oracle_index(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
-                           ctypes.byref(out), loff)
+    if threads > 1:
+        rc = L.ii_oracle_index_mt(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
+                                  threads, ctypes.byref(out), loff)
+    else:
+        rc = L.ii_oracle_index(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
+                               ctypes.byref(out), loff)
     assert rc == 0
     res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
     L.ii_oracle_free(out)

@@ -26,6 +26,22 @@ def test_layout():
             assert t[off[f + 1] - 1] in ws  # every file ends in whitespace (separator contract)
 
 
+def test_shard_equals_slices_of_the_corpus():
+    # a GPU's shard (bench.py strong scaling) is byte-identical to its files' slices of the whole corpus
+    t, off = ii_ctypes.zipf_corpus(2_000_000, 53, 3000, 11, threads=3)
+    assert (ii_ctypes.zipf_layout(2_000_000, 53, 11) == off).all()
+    sizes = [int(off[i + 1] - off[i]) for i in range(53)]
+    order, sb, se = ii_ctypes.partition(sizes, 4)
+    for g in range(4):
+        files = sorted(order[sb[g]:se[g]])
+        s, so = ii_ctypes.zipf_shard(2_000_000, 53, 3000, 11, files, threads=2)
+        exp = b"".join(t[int(off[f]):int(off[f + 1])].tobytes() for f in files)
+        assert s.tobytes() == exp
+        assert [int(x) for x in so[1:] - so[:-1]] == [sizes[f] for f in files]
+    s, so = ii_ctypes.zipf_shard(2_000_000, 53, 3000, 11, [], threads=2)
+    assert len(s) == 0 and list(so) == [0]
+
+
 def test_golden_zipf_corpus_reproduces():
     import json, os
     from conftest import GOLDEN

@@ -41,6 +41,17 @@ def test_cli_matches_reference(case):
         assert r.returncode == 0, r.stderr.decode()
         got = {l: open(os.path.join(td, l + ".txt"), "rb").read() for l in LETTERS}
         assert_same(got, expected, case)
+        # missing files: reported once each, by the mapper whose shard holds them (main.c:98, 290-296)
+        toks = open(os.path.join(td, "list.txt")).read().split()
+        paths = toks[1:1 + int(toks[0])]
+        sizes = [os.path.getsize(os.path.join(td, p)) if os.path.exists(os.path.join(td, p)) else 0 for p in paths]
+        order, sb, se = ii_ctypes.partition(sizes, 3)
+        err = r.stderr.decode()
+        for m in range(3):
+            for i in order[sb[m]:se[m]]:
+                if not os.path.exists(os.path.join(td, paths[i])):
+                    assert err.count("Mapper %d: Error opening file %s\n" % (m, paths[i])) == 1, err
+                    assert "Error getting size of file: %s\n" % paths[i] in err
 
 
 @pytest.mark.parametrize("case", CASES)

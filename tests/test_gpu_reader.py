@@ -58,11 +58,13 @@ def test_reader_missing_empty_shrunk_grown(idx, capfd):
                 exp_text += text[off[f]:off[f + 1]]
             exp_off.append(len(exp_text))
         exp = oracle_index(bytes(exp_text), exp_off, ids)
+        mappers = [(f * 7) % 5 for f in range(30)]  # file 3 belongs to mapper 1
         # exact sizes
-        idx.map_files(paths, nthreads=4, sizes=sizes)
+        idx.map_files(paths, nthreads=4, sizes=sizes, mappers=mappers)
         idx.reduce()
         assert_same(idx.letters(), exp, "exact")
-        assert "Error opening file %s" % paths[3] in capfd.readouterr().err
+        # the owning mapper's id, as main.c:98 prints it
+        assert "Mapper 1: Error opening file %s\n" % paths[3] in capfd.readouterr().err
         # sizes larger than the files: the reader pads with spaces
         idx.map_files(paths, nthreads=4, sizes=[s + 5000 for s in sizes])
         idx.reduce()
@@ -71,6 +73,9 @@ def test_reader_missing_empty_shrunk_grown(idx, capfd):
         small = list(sizes)
         small[7] = max(0, small[7] // 2)
         small[8] = 0
-        idx.map_files(paths, nthreads=4, sizes=small)
+        capfd.readouterr()
+        idx.map_files(paths, nthreads=4, sizes=small, mappers=mappers)
         idx.reduce()
         assert_same(idx.letters(), exp, "grown")
+        # reported once, although the fallback re-reads every file
+        assert capfd.readouterr().err.count("Error opening file %s" % paths[3]) == 1

@@ -20,6 +20,23 @@ def test_oracle_matches_reference_goldens(case):
         assert got[l] == expected[l], "letter %s differs" % l
 
 
+@pytest.mark.parametrize("threads", [2, 3, 8, 40])
+@pytest.mark.parametrize("case", ["config1", "config2", "edge", "rand_1", "tiny360", "zipf_small"])
+def test_multithreaded_oracle_matches_reference_goldens(case, threads):
+    # the full-size CPU baseline of bench.py (ii_oracle_index_mt), incl. more threads than files
+    text, off, ids, expected = case_arrays(case)
+    got = oracle_index(text, off, ids, threads=threads)
+    for l in "abcdefghijklmnopqrstuvwxyz":
+        assert got[l] == expected[l], "letter %s differs" % l
+
+
+def test_multithreaded_oracle_matches_single_thread_zipf():
+    import ii_ctypes
+    t, off = ii_ctypes.zipf_corpus(30_000_000, 500, 300_000, 4, threads=8)
+    ids = [2 * i + 1 for i in range(500)]
+    assert oracle_index(t, off, ids, threads=7) == oracle_index(t, off, ids)
+
+
 def test_golden_json_consistent():
     meta = json.load(open(os.path.join(GOLDEN, "golden.json")))
     # config 1 / config 2 aggregate hashes of the reference
