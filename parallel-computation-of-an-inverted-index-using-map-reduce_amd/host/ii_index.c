@@ -5,9 +5,21 @@
  *
  * Same argument handling, list format, file-ID numbering and outputs
  * (a.txt .. z.txt in the current directory) as /root/reference/main.c:246-390.
- * The map and reduce phases (main.c:326-384) run on the MI355X through
+ * The map and reduce phases (main.c:326-384) run on MI355X GPUs through
  * libii.so (include/ii.h); M sizes the host reader threads and R the writer
  * threads, neither changes the output.
+ *
+ * GPUs: II_GPUS=G (a number, or "all" = every visible device; default 1).
+ * With G > 1 the files are sharded over G contexts by the reference's own
+ * size heuristic (ii_partition, main.c:300-323), one host pthread per context
+ * maps and locally reduces its shard, the G contexts exchange letter ranges —
+ * the reference's reducer map with R = G (main.c:129-130), or histogram-
+ * balanced ranges with II_LETTER_SPLIT=balanced — and each
+ * owner merges, orders and formats its letters.  The exchange moves the
+ * export segments with ONE grouped RCCL ncclSend / ncclRecv round over xGMI
+ * when the G contexts sit on G distinct devices; when fewer devices are
+ * visible the contexts share them ("G logical shards") and the
+ * segments move by device copies.  Output is identical for every G.
  *
  * With II_PARTIAL_FILES=1 in the environment the CLI also leaves the
  * reference's partial_<letter>.txt files in the current directory
@@ -23,10 +35,46 @@
 #include <string.h>
 #include <sys/stat.h>
 
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
 #include "ii.h"
 
+#define MAXG II_MAX_PARTS
+
+/* One GPU context of the multi-GPU CLI and its shard of files. */
 typedef struct {
+    int dev, nparts;
     ii_ctx *ctx;
+    ii_file *files;   /* the shard's files, ascending id0 */
+    uint32_t n;
+    uint32_t *local;  /* list index -> index in this shard (UINT32_MAX: another shard) */
+    int nthreads;
+    int rc;
+    /* exchange: segment bytes for every owner, send / receive offsets */
+    uint64_t seg[MAXG], send_off[MAXG + 1], recv_off[MAXG + 1];
+    void *d_send, *d_recv;
+    uint32_t id_bound;
+    hipStream_t st;
+} shard;
+
+/* ---- phase bodies, one pthread per context */
+static void *map_body(void *p) {
+    shard *s = p;
+    s->rc = ii_open(&s->ctx, s->dev);
+    if (s->rc == II_OK) s->rc = ii_map_files(s->ctx, s->files, s->n, s->nthreads, NULL);
+    if (s->rc == II_OK) s->rc = ii_reduce_local(s->ctx); /* lexid-keyed partial index, letter-contiguous */
+    return NULL;
+}
+static void *merge_body(void *p) {
+    shard *s = p;
+    s->rc = ii_import(s->ctx, s->nparts, s->d_recv, s->recv_off, s->id_bound);
+    if (s->rc == II_OK) s->rc = ii_reduce(s->ctx, 1);
+    return NULL;
+}
+
+typedef struct {
+    ii_ctx **owner;  /* context holding each letter's text */
     int r, R;
     int err;
 } writer_arg;
@@ -42,13 +90,216 @@ static void *writer(void *p) {
         size_t len;
         char name[16];
         snprintf(name, sizeof(name), "%c.txt", 'a' + l);
-        if (ii_letter_text(w->ctx, l, &buf, &len) != II_OK) { w->err = 1; continue; }
+        if (ii_letter_text(w->owner[l], l, &buf, &len) != II_OK) { w->err = 1; continue; }
         FILE *o = fopen(name, "w");
         if (!o) { printf("eroare la fisierul final\n"); w->err = 1; continue; } /* main.c:151-154 */
         if (len && fwrite(buf, 1, len, o) != len) w->err = 1;
         fclose(o);
     }
     return NULL;
+}
+
+static int gpus_requested(void) {
+    const char *e = getenv("II_GPUS");
+    if (!e || !*e) return 1;
+    if (!strcmp(e, "all")) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return 1;
+        return n > MAXG ? MAXG : n;
+    }
+    int g = atoi(e);
+    return g < 1 ? 1 : g > MAXG ? MAXG : g;
+}
+
+/* Move segment (g -> r) of every pair: one grouped RCCL round when every
+ * shard has a device of its own (point-to-point over xGMI, all pairs at
+ * once), device copies when shards share devices. */
+static int exchange(shard *sh, int G, int distinct) {
+    if (distinct) {
+        ncclComm_t comms[MAXG];
+        int devs[MAXG];
+        for (int g = 0; g < G; g++) devs[g] = sh[g].dev;
+        if (ncclCommInitAll(comms, G, devs) != ncclSuccess) return II_ERR_HIP;
+        int bad = 0;
+        for (int g = 0; g < G; g++) {
+            bad |= hipSetDevice(sh[g].dev) != hipSuccess;
+            bad |= hipStreamCreateWithFlags(&sh[g].st, hipStreamNonBlocking) != hipSuccess;
+        }
+        bad |= ncclGroupStart() != ncclSuccess;
+        for (int g = 0; g < G && !bad; g++)
+            for (int r = 0; r < G && !bad; r++) {
+                const uint64_t n = sh[g].seg[r];
+                if (!n) continue;
+                /* rank g sends its segment for owner r; owner r receives it at source g's offset */
+                bad |= ncclSend((const char *)sh[g].d_send + sh[g].send_off[r], n, ncclUint8, r, comms[g],
+                                sh[g].st) != ncclSuccess;
+                bad |= ncclRecv((char *)sh[r].d_recv + sh[r].recv_off[g], n, ncclUint8, g, comms[r],
+                                sh[r].st) != ncclSuccess;
+            }
+        bad |= ncclGroupEnd() != ncclSuccess;
+        for (int g = 0; g < G; g++) {
+            bad |= hipSetDevice(sh[g].dev) != hipSuccess;
+            bad |= hipStreamSynchronize(sh[g].st) != hipSuccess;
+            (void)hipStreamDestroy(sh[g].st);
+            ncclCommDestroy(comms[g]);
+        }
+        return bad ? II_ERR_HIP : II_OK;
+    }
+    for (int g = 0; g < G; g++)
+        for (int r = 0; r < G; r++) {
+            const uint64_t n = sh[g].seg[r];
+            if (!n) continue;
+            if (hipMemcpyPeer((char *)sh[r].d_recv + sh[r].recv_off[g], sh[r].dev,
+                              (const char *)sh[g].d_send + sh[g].send_off[r], sh[g].dev, n) != hipSuccess)
+                return II_ERR_HIP;
+        }
+    for (int g = 0; g < G; g++)
+        if (hipSetDevice(sh[g].dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return II_ERR_HIP;
+    return II_OK;
+}
+
+/* Multi-context index (G > 1), first half: shard the files, then map +
+ * local reduce every shard (one pthread per context). */
+static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count, int M, int G, shard *sh) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
+    uint32_t *order = calloc((size_t)count + 1, sizeof(uint32_t));
+    uint32_t *shard_of = calloc((size_t)count + 1, sizeof(uint32_t));
+    uint32_t sb[MAXG], se[MAXG];
+    ii_partition(sizes, count, G, order, sb, se); /* main.c:300-323 with M = G */
+    for (int g = 0; g < G; g++)
+        for (uint32_t j = sb[g]; j < se[g]; j++) shard_of[order[j]] = (uint32_t)g;
+    for (int g = 0; g < G; g++) {
+        sh[g].dev = g % ndev;
+        sh[g].nparts = G;
+        sh[g].n = 0;
+        sh[g].files = calloc((size_t)(se[g] - sb[g]) + 1, sizeof(ii_file));
+        sh[g].local = malloc(((size_t)count + 1) * sizeof(uint32_t));
+        sh[g].nthreads = M / G > 0 ? M / G : 1;
+        sh[g].id_bound = count;
+    }
+    /* every shard in ascending id0 = list order (ii_map_files requires it; postings come out ascending) */
+    for (uint32_t i = 0; i < count; i++)
+        for (int g = 0; g < G; g++) {
+            if (shard_of[i] == (uint32_t)g) {
+                sh[g].local[i] = sh[g].n;
+                sh[g].files[sh[g].n++] = files[i];
+            } else {
+                sh[g].local[i] = UINT32_MAX;
+            }
+        }
+    free(order);
+    free(shard_of);
+    int rc = II_OK;
+    pthread_t th[MAXG];
+    for (int g = 0; g < G; g++) pthread_create(&th[g], NULL, map_body, &sh[g]);
+    for (int g = 0; g < G; g++) {
+        pthread_join(th[g], NULL);
+        if (sh[g].rc != II_OK && rc == II_OK) rc = sh[g].rc;
+    }
+    return rc;
+}
+
+/* Second half: letter owners, export, exchange, merge, order + format.
+ * owner[l] receives the context holding letter l. */
+static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
+    const int distinct = ndev >= G;
+    int rc = II_OK;
+    pthread_t th[MAXG];
+
+    /* letter owners */
+    int lo[MAXG], hi[MAXG];
+    const char *split = getenv("II_LETTER_SPLIT");
+    if (split && !strcmp(split, "balanced")) {
+        uint64_t load[II_ALPHABET] = {0}, part[II_ALPHABET];
+        for (int g = 0; g < G; g++) {
+            if ((rc = ii_letter_load(sh[g].ctx, part)) != II_OK) return rc;
+            for (int l = 0; l < II_ALPHABET; l++) load[l] += part[l];
+        }
+        if ((rc = ii_balanced_letters(load, G, lo, hi)) != II_OK) return rc;
+    } else {
+        for (int r = 0; r < G; r++) ii_reducer_letters(r, G, &lo[r], &hi[r]); /* main.c:129-130 */
+    }
+    for (int r = 0; r < G; r++)
+        for (int l = lo[r]; l < hi[r]; l++) owner[l] = sh[r].ctx;
+
+    /* plans, buffers, export */
+    for (int g = 0; g < G; g++) {
+        if ((rc = ii_export_plan_ranges(sh[g].ctx, G, lo, hi, sh[g].seg)) != II_OK) return rc;
+        sh[g].send_off[0] = 0;
+        for (int r = 0; r < G; r++) sh[g].send_off[r + 1] = sh[g].send_off[r] + sh[g].seg[r];
+    }
+    for (int r = 0; r < G; r++) {
+        sh[r].recv_off[0] = 0;
+        for (int g = 0; g < G; g++) sh[r].recv_off[g + 1] = sh[r].recv_off[g] + sh[g].seg[r];
+    }
+    for (int g = 0; g < G; g++) {
+        if (hipSetDevice(sh[g].dev) != hipSuccess) return II_ERR_HIP;
+        if (hipMalloc(&sh[g].d_send, sh[g].send_off[G] + 8) != hipSuccess ||
+            hipMalloc(&sh[g].d_recv, sh[g].recv_off[G] + 8) != hipSuccess)
+            return II_ERR_NOMEM;
+        if ((rc = ii_export(sh[g].ctx, G, sh[g].d_send, sh[g].send_off)) != II_OK) return rc;  /* synchronous */
+    }
+    if ((rc = exchange(sh, G, distinct)) != II_OK) return rc;
+
+    /* owners: merge the received segments, order + format (one thread per context) */
+    for (int g = 0; g < G; g++) pthread_create(&th[g], NULL, merge_body, &sh[g]);
+    for (int g = 0; g < G; g++) {
+        pthread_join(th[g], NULL);
+        if (sh[g].rc != II_OK && rc == II_OK) rc = sh[g].rc;
+    }
+    for (int g = 0; g < G; g++) {
+        (void)hipSetDevice(sh[g].dev);
+        (void)hipFree(sh[g].d_send);
+        (void)hipFree(sh[g].d_recv);
+        sh[g].d_send = sh[g].d_recv = NULL;
+    }
+    return rc;
+}
+
+/* partial_<letter>.txt (main.c:332-341): emit[] lists the files in the
+ * reference's emission order (mapper 0's, then mapper 1's, ...); with G
+ * contexts every run of consecutive files held by one context is appended in
+ * turn. */
+static int write_partials(shard *sh, int G, ii_ctx *single, const uint32_t *emit, uint32_t n) {
+    FILE *out[II_ALPHABET];
+    for (int l = 0; l < II_ALPHABET; l++) {
+        char name[32];
+        snprintf(name, sizeof(name), "partial_%c.txt", 'a' + l);
+        out[l] = fopen(name, "w+");
+        if (!out[l]) {
+            fprintf(stderr, "Error creating partial file: %s\n", name); /* main.c:336 */
+            for (int k = 0; k < l; k++) fclose(out[k]);
+            return II_ERR_IO;
+        }
+    }
+    int rc = II_OK;
+    uint32_t *run = malloc(((size_t)n + 1) * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n && rc == II_OK;) {
+        ii_ctx *ctx = single;
+        uint32_t k = 0, j = i;
+        if (single) {
+            for (; j < n; j++) run[k++] = emit[j];
+        } else {
+            int g = 0;
+            while (sh[g].local[emit[i]] == UINT32_MAX) g++;
+            ctx = sh[g].ctx;
+            for (; j < n && sh[g].local[emit[j]] != UINT32_MAX; j++) run[k++] = sh[g].local[emit[j]];
+        }
+        i = j;
+        rc = ii_partials(ctx, run, k);
+        for (int l = 0; rc == II_OK && l < II_ALPHABET; l++) {
+            const char *buf;
+            size_t len;
+            rc = ii_partial_text(ctx, l, &buf, &len);
+            if (rc == II_OK && len && fwrite(buf, 1, len, out[l]) != len) rc = II_ERR_IO;
+        }
+    }
+    free(run);
+    for (int l = 0; l < II_ALPHABET; l++) fclose(out[l]);
+    return rc;
 }
 
 int main(int argc, char **argv) {
@@ -103,43 +354,41 @@ int main(int argc, char **argv) {
         printf("Mapper %d: Files %u to %u\n", m, sb[m], se[m]);
         for (uint32_t i = sb[m]; i < se[m]; i++) files[order[i]].mapper = m; /* main.c:98 names it */
     }
-
-    ii_ctx *ctx = NULL;
-    int rc = ii_open(&ctx, 0);
-    if (rc != II_OK) {
-        fprintf(stderr, "ii_index: cannot open device: %s\n", ii_strerror(rc));
-        return 1;
-    }
-    /* files in list (= ID) order: postings come out ascending (main.c:217-226) */
-    rc = ii_map_files(ctx, files, (uint32_t)count, M, NULL);
+    /* the reference's emission order of the partial files: mapper 0's files, then mapper 1's, ... */
+    uint32_t nemit = 0;
+    for (int m = 0; m < M; m++)
+        for (uint32_t i = sb[m]; i < se[m]; i++) order[nemit++] = order[i];
     const char *pe = getenv("II_PARTIAL_FILES");
-    if (rc == II_OK && pe && atoi(pe) == 1) {
-        /* mapper m reads order[sb[m] .. se[m]) (main.c:93); mappers one after another */
-        uint32_t n = 0;
-        for (int m = 0; m < M; m++)
-            for (uint32_t i = sb[m]; i < se[m]; i++) order[n++] = order[i];
-        rc = ii_partials(ctx, order, n);
-        for (int l = 0; rc == II_OK && l < 26; l++) {
-            const char *buf;
-            size_t len;
-            char name[32];
-            snprintf(name, sizeof(name), "partial_%c.txt", 'a' + l);
-            rc = ii_partial_text(ctx, l, &buf, &len);
-            if (rc != II_OK) break;
-            FILE *o = fopen(name, "w+");
-            if (!o) {
-                fprintf(stderr, "Error creating partial file: %s\n", name); /* main.c:336 */
-                rc = II_ERR_IO;
-                break;
-            }
-            if (len && fwrite(buf, 1, len, o) != len) rc = II_ERR_IO;
-            fclose(o);
+    const int partials = pe && atoi(pe) == 1;
+
+    const int G = gpus_requested();
+    ii_ctx *owner[II_ALPHABET];
+    ii_ctx *single = NULL;
+    shard sh[MAXG];
+    memset(sh, 0, sizeof(sh));
+    int rc;
+    if (G == 1) {
+        rc = ii_open(&single, 0);
+        if (rc != II_OK) {
+            fprintf(stderr, "ii_index: cannot open device: %s\n", ii_strerror(rc));
+            return 1;
         }
+        /* files in list (= ID) order: postings come out ascending (main.c:217-226) */
+        rc = ii_map_files(single, files, (uint32_t)count, M, NULL);
+        if (rc == II_OK && partials) rc = write_partials(NULL, 0, single, order, nemit);
+        if (rc == II_OK) rc = ii_reduce(single, 1);
+        for (int l = 0; l < II_ALPHABET; l++) owner[l] = single;
+    } else {
+        rc = multi_map(files, sizes, (uint32_t)count, M, G, sh);
+        /* partial files while the contexts still hold their input files (before the exchange) */
+        if (rc == II_OK && partials) rc = write_partials(sh, G, NULL, order, nemit);
+        if (rc == II_OK) rc = multi_exchange(G, sh, owner);
     }
-    if (rc == II_OK) rc = ii_reduce(ctx, 1);
     if (rc != II_OK) {
         fprintf(stderr, "ii_index: %s\n", ii_strerror(rc));
-        ii_close(ctx);
+        if (single) ii_close(single);
+        for (int g = 0; g < G; g++)
+            if (sh[g].ctx) ii_close(sh[g].ctx);
         return 1;
     }
     int err = 0;
@@ -147,7 +396,7 @@ int main(int argc, char **argv) {
         pthread_t *th = calloc((size_t)R, sizeof(pthread_t));
         writer_arg *wa = calloc((size_t)R, sizeof(writer_arg));
         for (int r = 0; r < R; r++) {
-            wa[r] = (writer_arg){ctx, r, R, 0};
+            wa[r] = (writer_arg){owner, r, R, 0};
             pthread_create(&th[r], NULL, writer, &wa[r]);
         }
         for (int r = 0; r < R; r++) {
@@ -157,7 +406,12 @@ int main(int argc, char **argv) {
         free(th);
         free(wa);
     }
-    ii_close(ctx);
+    if (single) ii_close(single);
+    for (int g = 0; g < G; g++) {
+        if (sh[g].ctx) ii_close(sh[g].ctx);
+        free(sh[g].files);
+        free(sh[g].local);
+    }
     for (int i = 0; i < count; i++) free(names[i]);
     free(names);
     free(files);

@@ -1,0 +1,56 @@
+"""GPU: the drop-in CLI over several GPU contexts (II_GPUS=G):
+files sharded by the reference's size heuristic (main.c:300-323), one host
+pthread per context, letter ranges exchanged (the reference's reducer map
+with R = G, main.c:129-130, or II_LETTER_SPLIT=balanced) — against every
+reference golden.  With one visible device the G contexts share it and the
+segments move by device copies; on a node with >= G devices the same code
+path moves them with grouped RCCL send / recv."""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import CASES, PKG, materialize, partials_meta
+from test_gpu_parity import LETTERS, assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def run_cli(case, M, R, env_extra):
+    with tempfile.TemporaryDirectory() as td:
+        _, _, expected = materialize(case, td)
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([os.path.join(PKG, "ii_index"), str(M), str(R), "list.txt"], cwd=td, capture_output=True,
+                           timeout=180, env=env)
+        assert r.returncode == 0, r.stderr.decode()
+        got = {l: open(os.path.join(td, l + ".txt"), "rb").read() for l in LETTERS}
+        parts = {l: open(os.path.join(td, "partial_%s.txt" % l), "rb").read() for l in LETTERS} \
+            if env_extra.get("II_PARTIAL_FILES") == "1" else None
+        return got, expected, parts, r
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_cli_three_gpus_matches_reference(case):
+    got, expected, _, r = run_cli(case, 4, 5, {"II_GPUS": "3"})
+    assert_same(got, expected, "%s II_GPUS=3" % case)
+    assert r.stdout.decode().count("REDUCER\n") == 5
+
+
+@pytest.mark.parametrize("case,G,split", [("config2", 2, "reference"), ("config2", 8, "balanced"),
+                                          ("zipf_small", 5, "balanced"), ("edge", 7, "reference"),
+                                          ("tiny360", 4, "balanced"), ("rand_2", 26, "reference")])
+def test_cli_gpu_counts_and_letter_splits(case, G, split):
+    got, expected, _, _ = run_cli(case, 3, 26, {"II_GPUS": str(G), "II_LETTER_SPLIT": split})
+    assert_same(got, expected, "%s II_GPUS=%d %s" % (case, G, split))
+
+
+@pytest.mark.parametrize("case", ["config1", "edge", "zipf_small"])
+def test_cli_multi_gpu_partial_files(case):
+    # M = 1: the reference's own partial files, byte for byte, although the files live on 3 contexts
+    got, expected, parts, _ = run_cli(case, 1, 2, {"II_GPUS": "3", "II_PARTIAL_FILES": "1"})
+    assert_same(got, expected, case)
+    meta = partials_meta()[case]
+    for l in LETTERS:
+        assert hashlib.sha256(parts[l]).hexdigest() == meta[l]["sha256"], "%s partial_%s.txt differs" % (case, l)
