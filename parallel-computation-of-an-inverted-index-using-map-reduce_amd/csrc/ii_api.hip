@@ -18,9 +18,6 @@
 #include "ii_kernels.h"
 #include "ii_partial.h"
 
-#ifndef II_LV_BLOCKS
-#define II_LV_BLOCKS 8192  // grid cap of k_long_verify (grid-stride loop)
-#endif
 
 using namespace ii;
 
@@ -475,6 +472,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         return II_OK;
     }
     const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
+    const uint32_t wg_chunks = (uint32_t)((nch + kWG - 1) / kWG);  // K1 kernels: one wave per chunk
     c->nch_map = nch;
     CK(grow(c->chunk_cnt, sizeof(uint64_t) * (nch + 1)));
     CK(grow(c->chunk_hist, sizeof(uint32_t) * 26 * nch));
@@ -493,7 +491,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
         c->T = 0;
     } else {
-        k_tok_count<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, chunk_cnt);
+        k_tok_count<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, chunk_cnt);
         CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
         CK(read_u64(c, totals, &hv[0]));
         CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
@@ -521,36 +519,38 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
-        k_tok_emit<0><<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
+        k_tok_emit<0><<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, fid, chunk_cnt,
                                                        c->rec_cap, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
                                                        P_<uint32_t>(c->chunk_files));
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
-        k_tok_resolve<<<(uint32_t)nch, kBlock, 0, c->st>>>(c->text, c->nbytes, fstart, fid, c->nfiles, chunk_cnt,
+        k_tok_resolve<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, fid, chunk_cnt,
                                                            c->rec_cap, P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
                                                            P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                           P_<LongTok>(c->longs), c->long_cap, P_<uint32_t>(c->chunk_files));
+                                                           P_<LongTok>(c->longs), c->long_cap / kLongShards,
+                                                           P_<uint32_t>(c->chunk_files));
+        k_long_totals<<<1, 64, 0, c->st>>>(counters);
         HIPCK(hipEventRecord(c->ev_res[1], c->st));
         CK(run_reduce(c, OpU32{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
-        uint64_t cnt[4];
-        CK(read_u64(c, counters, cnt, 4));
+        uint64_t cnt[C_LONGMAX + 1];
+        CK(read_u64(c, counters, cnt, C_LONGMAX + 1));
         if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] > kHotSlots / 2 + c->big_cap / 2) {
             c->big_cap *= 4;
             c->retries++;
             continue;
         }
         if (cnt[C_OVERFLOW] & 2) {
-            c->long_cap = cnt[C_LONG] + cnt[C_LONG] / 4 + 1024;
+            c->long_cap = (uint64_t)kLongShards * (cnt[C_LONGMAX] + cnt[C_LONGMAX] / 4 + 1024);
             c->retries++;
             continue;
         }
         c->nlong = cnt[C_LONG];
         if (c->nlong) {
-            uint32_t g = (uint32_t)std::min<uint64_t>(II_LV_BLOCKS, grid_for(c->nlong));
-            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->nlong,
+            const dim3 g(kLongShards, (uint32_t)std::min<uint64_t>(128, grid_for(cnt[C_LONGMAX])));
+            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->long_cap / kLongShards,
                                                  P_<uint64_t>(c->trep), counters);
             HIPCK(hipGetLastError());
             CK(read_u64(c, counters, cnt, 4));

@@ -17,10 +17,7 @@
 namespace ii {
 
 // ---------------------------------------------------------------- constants
-constexpr int kTile = 4096;        // bytes staged per tokenizer step (256 lanes x 16 B)
-constexpr int kHalo = 512;         // right halo staged with each tile
-constexpr int kChunkTiles = 16;    // tiles per tokenizer workgroup
-constexpr uint64_t kChunk = (uint64_t)kTile * kChunkTiles;  // 64 KiB of text per workgroup
+constexpr uint64_t kChunk = 16384;  // bytes of text per K1 chunk (one wave each, see "K1 chunks")
 constexpr int kMaxWord = 299;      // MAX_WORD - 1 letters (main.c:7, 105)
 constexpr int kMaxProbe = 1 << 14;
 
@@ -35,8 +32,14 @@ enum : int {
     C_HIST = 4,      // 26 first-letter counters
     C_TIES = 30,     // dictionary entries sharing a 12-letter prefix
     C_MAXLEN = 31,   // longest tied word
-    C_NUM = 32
+    C_LONGMAX = 32,  // fullest long-token queue shard
+    C_LSHARD = 40,   // kLongShards queue counters, 16 apart (one 128-B line each)
+    C_NUM = 40 + 64 * 16
 };
+// Long tokens are queued in kLongShards shards (by chunk) so that the
+// queue's atomics do not all hit one address: one word saturates at about
+// 90 atomics per microsecond (MI355X_MICROARCH.md, fanin / dequeue rows).
+constexpr int kLongShards = 64;
 
 // C-locale isspace: the fscanf("%s") delimiter set (main.c:102).
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == 32u || (c - 9u) < 5u; }
@@ -198,31 +201,14 @@ struct TileReader {
     }
 };
 
-// Cleaning loop of main.c:105-111 from tile-local byte p: stops at whitespace,
-// NUL or the 299th letter.  Returns the word key (exact 5-bit packing for
-// <= 12 letters, tagged hash otherwise) and its letter count (0 = dropped).
+// Word key of a token (the cleaning loop of main.c:105-111): exact 5-bit
+// packing for <= 12 letters, tagged hash otherwise; its letter count (0 =
+// dropped, main.c:113) and first letter.
 struct TokKey {
     uint64_t key;
     uint32_t nlet;
     uint32_t first;
 };
-__device__ __forceinline__ TokKey token_key(TileReader& rd, uint32_t p, uint64_t seed) {
-    uint64_t packed = 0, hash = 1469598103934665603ull;
-    uint32_t n = 0, first = 0;
-    for (uint32_t j = p;; j++) {
-        const uint32_t c = rd.get(j);
-        if (c == 0u || is_ws(c)) break;
-        const uint32_t lc = letter_of(c);
-        if (lc < 26u) {
-            if (n == 0) first = lc;
-            n++;
-            if (n <= 12) packed |= (uint64_t)(lc + 1) << (64 - 5 * n);
-            hash = (hash ^ (lc + 1)) * 1099511628211ull;
-            if (n == (uint32_t)kMaxWord) break;
-        }
-    }
-    return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
-}
 
 // A token is kept iff a letter comes before the first whitespace / NUL
 // (main.c:105, 113).  Cheap form for the count pass.
@@ -262,50 +248,28 @@ __global__ __launch_bounds__(kBlock) void k_chunk_files(const uint64_t* __restri
     cf[3 * c + 2] = file_id[f0];
 }
 
+// The 16 bytes at g, a multiple of 16 (the text is 16-byte aligned); bytes
+// outside [0, nbytes) read as ' '.  An aligned 16-B block never straddles a
+// page, so once its first byte is text the whole load is safe; the bytes past
+// the end are replaced (no per-byte path: it would cost every caller's
+// registers).
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int64_t left) {
+    if (left >= 4) return w;
+    if (left <= 0) return 0x20202020u;
+    const uint32_t m = (1u << (8 * (uint32_t)left)) - 1u;
+    return (w & m) | (0x20202020u & ~m);
+}
 __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, uint64_t nbytes, int64_t g) {
-    if (g >= 0 && (uint64_t)g + 16 <= nbytes) return *reinterpret_cast<const uint4*>(text + g);
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const int64_t gi = g + i;
-        const uint32_t b = (gi >= 0 && (uint64_t)gi < nbytes) ? text[gi] : 32u;
-        w[i >> 2] |= b << ((i & 3) * 8);
+    if (g < 0 || (uint64_t)g >= nbytes) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    uint4 v = *reinterpret_cast<const uint4*>(text + g);
+    const int64_t left = (int64_t)(nbytes - (uint64_t)g);
+    if (left < 16) {
+        v.x = keep_bytes(v.x, left);
+        v.y = keep_bytes(v.y, left - 4);
+        v.z = keep_bytes(v.z, left - 8);
+        v.w = keep_bytes(v.w, left - 12);
     }
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// Tile staging, software-pipelined: fetch_tile() loads the text of
-// [tile_lo - 16, tile_lo + kTile + kHalo) into registers (16 B per lane; lane
-// t's own window [tile_lo + 16t, +16) in .v, the left piece and the halo in
-// .h of lanes 0..32) one tile ahead; store_tile() writes them to LDS.  Bytes
-// outside the text read as ' ' (so position 0 starts a token).
-struct TileRegs {
-    uint4 v, h;
-};
-constexpr int kExtraPieces = 1 + kHalo / 16;  // left piece + halo pieces
-__device__ __forceinline__ TileRegs fetch_tile(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t tile_lo) {
-    const int t = threadIdx.x;
-    TileRegs r;
-    r.v = load16(text, nbytes, (int64_t)tile_lo + 16 * t);
-    r.h = make_uint4(0, 0, 0, 0);
-    if (t < kExtraPieces) {
-        const int q = t == 0 ? -1 : kTile / 16 + t - 1;
-        r.h = load16(text, nbytes, (int64_t)tile_lo + 16 * q);
-    }
-    return r;
-}
-__device__ __forceinline__ void store_tile(uint8_t* s_text, const TileRegs& r) {
-    const int t = threadIdx.x;
-    *reinterpret_cast<uint4*>(s_text + 16 + 16 * t) = r.v;
-    if (t < kExtraPieces) {
-        const int q = t == 0 ? -1 : kTile / 16 + t - 1;
-        *reinterpret_cast<uint4*>(s_text + 16 + 16 * q) = r.h;
-    }
-}
-
-__device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {
-    const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
-    return (w >> ((i & 3) * 8)) & 0xFFu;
+    return v;
 }
 
 // ---- SWAR byte classes, 4 bytes per u32 (exact, no inter-byte carries)
@@ -344,23 +308,12 @@ __device__ __forceinline__ Classes classify16(const uint4& v) {
     return c;
 }
 
-// Token starts of the lane's window (non-space after space, main.c:102).  The
-// byte before the window comes from the neighbour lane (LDS for lane 0 of a
-// wave).  Call after the staging barrier.
-__device__ __forceinline__ uint32_t lane_starts(const uint4& v, const Classes& cl, const uint8_t* s_text) {
-    const int t = threadIdx.x;
-    uint32_t prev = __shfl_up(v.w, 1, 64) >> 24;
-    if ((t & 63) == 0) prev = s_text[16 + 16 * t - 1];
-    const uint32_t prev_ws = is_ws(prev) ? 1u : 0u;
-    return ~cl.ws & ((cl.ws << 1) | prev_ws) & 0xFFFFu;
-}
-
 // Kept tokens among the starts (a letter before the first whitespace / NUL,
 // main.c:105, 113); decided from the masks, walking LDS only when the window
 // ends before the token shows a letter, space or NUL.
 __device__ __forceinline__ uint32_t kept_starts(uint32_t starts, const Classes& cl, const uint8_t* s_text,
                                                 const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t tile_lo,
-                                                uint32_t wlo, uint32_t lim = kTile + kHalo) {
+                                                uint32_t wlo, uint32_t lim) {
     const uint32_t ev = cl.letter | cl.ws | cl.nul;
     uint32_t kept = 0;
     for (uint32_t m = starts & ~cl.letter; m; m &= m - 1) {  // starts that are not letters themselves
@@ -391,29 +344,6 @@ __device__ __forceinline__ uint4 token_bytes(const uint32_t (&w)[8], uint32_t i)
     for (int j = 0; j < 5; j++) x[j] = sel4(wo, w[j], w[j + 1], w[j + 2], w[j + 3]);
     return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], bo), __builtin_amdgcn_alignbyte(x[2], x[1], bo),
                       __builtin_amdgcn_alignbyte(x[3], x[2], bo), __builtin_amdgcn_alignbyte(x[4], x[3], bo));
-}
-
-// Register fast path of the cleaning loop (main.c:105-111) for the common
-// token: it ends (whitespace / NUL) inside its first 16 bytes and its letters
-// form one run from its first byte (plain or capitalised words, trailing
-// punctuation) with at most 12 letters.  Returns false otherwise.
-__device__ __forceinline__ bool fast_key(const uint4& tb, TokKey& out) {
-    const Classes c = classify16(tb);
-    const uint32_t term = c.ws | c.nul;
-    if (term == 0) return false;
-    const uint32_t e = __builtin_ctz(term);
-    const uint32_t lm = c.letter & ((1u << e) - 1u);
-    const uint32_t n = __popc(lm);
-    if (n == 0 || n > 12 || lm != (1u << n) - 1u) return false;
-    const uint32_t w[3] = {(tb.x | 0x20202020u) & 0x1F1F1F1Fu, (tb.y | 0x20202020u) & 0x1F1F1F1Fu,
-                           (tb.z | 0x20202020u) & 0x1F1F1F1Fu};
-    uint64_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 12; k++) packed |= (uint64_t)((w[k >> 2] >> (8 * (k & 3))) & 31u) << (59 - 5 * k);
-    out.key = packed & (~0ull << (64 - 5 * n));
-    out.nlet = n;
-    out.first = (w[0] & 31u) - 1u;
-    return true;
 }
 
 // 16 bytes of the text at any position g, from two aligned 16-B loads.
@@ -473,48 +403,82 @@ __device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, co
     return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
 }
 
-// K1a: kept tokens per 64 KiB chunk -> chunk_cnt[blockIdx.x], straight from
-// HBM (no LDS staging): lane t classifies windows w = 256 j + t of the chunk
-// with 16-B loads; the byte before a window comes from the neighbour lane, or
-// a 1-byte load for lane 0 of a wave; the rare start whose keep decision lies
-// past its window walks the text in HBM (kept_starts with nothing staged).
-// kept tokens among the starts of the 16-B window v at text position g
+// ---------------------------------------------------------------- K1 chunks
+// The text is cut into chunks of kChunk bytes, ONE WAVE per chunk (kWG
+// chunks per workgroup): a wave walks its chunk alone, with wave-level
+// ballots / scans and wave-private LDS, and never waits at a workgroup
+// barrier — the waves of a CU drift apart and overlap each other's memory
+// latency instead of meeting at a barrier every round.
+constexpr int kWG = kBlock / 64;  // chunks (waves) per workgroup
+
+// This wave's chunk, as a wave-uniform (scalar) value: the compiler cannot
+// prove threadIdx.x / 64 uniform, and everything derived from it would
+// otherwise live in vector registers.
+__device__ __forceinline__ uint64_t wave_chunk() {
+    return (uint64_t)blockIdx.x * kWG + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// Orders this wave's earlier LDS accesses before its later ones (LDS
+// instructions of one wave execute in program order; this keeps the compiler
+// from moving them across).  Not a workgroup barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+        if (lane_id() >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+// K1a: kept tokens per chunk -> chunk_cnt[c] (dense record layout only),
+// straight from HBM: lane l classifies windows 64 j + l of the chunk with
+// 16-B loads; the byte before a window comes from the neighbour lane, or a
+// 1-byte load for lane 0; the rare start whose keep decision lies past its
+// window walks the text in HBM (kept_starts with nothing staged).
 __device__ __forceinline__ uint32_t window_kept(const uint4& v, uint64_t g, const uint8_t* __restrict__ text,
                                                 uint64_t nbytes) {
     const Classes cl = classify16(v);
     uint32_t prev = (uint32_t)__shfl_up((int)v.w, 1, 64) >> 24;
-    if ((threadIdx.x & 63) == 0) prev = (g > 0 && g - 1 < nbytes) ? text[g - 1] : 32u;
+    if (lane_id() == 0) prev = (g > 0 && g - 1 < nbytes) ? text[g - 1] : 32u;
     const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
     return __popc(kept_starts(starts, cl, nullptr, text, nbytes, g, 0, 0));
 }
 
-__global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes,
+__global__ __launch_bounds__(kBlock) void k_tok_count(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                       uint64_t* __restrict__ chunk_cnt) {
-    __shared__ uint64_t s_scan[kWaves + 1];
-    constexpr int kWinsPerLane = (int)(kChunk / 16 / kBlock);
+    constexpr int kWinsPerLane = (int)(kChunk / 16 / 64);
     constexpr int kInFlight = 8;
-    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
-    const int t = threadIdx.x;
-    uint64_t kept = 0;
+    const uint64_t c = wave_chunk();
+    if (c >= nch) return;
+    const uint64_t chunk_lo = c * kChunk;
+    const int l = lane_id();
+    uint32_t kept = 0;
     if (chunk_lo + kChunk + 16 <= nbytes) {  // interior chunk: plain 16-B loads, 8 in flight per lane
         for (int jb = 0; jb < kWinsPerLane; jb += kInFlight) {
             uint4 v[kInFlight];
 #pragma unroll
             for (int u = 0; u < kInFlight; u++)
-                v[u] = *reinterpret_cast<const uint4*>(text + chunk_lo + 16 * ((uint64_t)kBlock * (jb + u) + t));
+                v[u] = *reinterpret_cast<const uint4*>(text + chunk_lo + 16 * (64ull * (jb + u) + l));
 #pragma unroll
-            for (int u = 0; u < kInFlight; u++)
-                kept += window_kept(v[u], chunk_lo + 16 * ((uint64_t)kBlock * (jb + u) + t), text, nbytes);
+            for (int u = 0; u < kInFlight; u++) kept += window_kept(v[u], chunk_lo + 16 * (64ull * (jb + u) + l), text, nbytes);
         }
     } else {
         for (int j = 0; j < kWinsPerLane; j++) {
-            const uint64_t g = chunk_lo + 16 * ((uint64_t)kBlock * j + t);
+            const uint64_t g = chunk_lo + 16 * (64ull * j + l);
             kept += window_kept(load16(text, nbytes, (int64_t)g), g, text, nbytes);
         }
     }
-    uint64_t tot;
-    (void)block_excl_scan(kept, &tot, s_scan);
-    if (t == 0) chunk_cnt[blockIdx.x] = tot;
+    kept = wave_sum32(kept);
+    if (l == 0) chunk_cnt[c] = kept;
 }
 
 // Long token queued for the exactness check (k_long_verify).
@@ -522,79 +486,80 @@ struct LongTok {
     uint64_t pos;   // token start
     uint64_t slot;  // word-table slot it was given
 };
-constexpr int kLongBuf = 128;  // per-workgroup LDS buffer of long tokens
 
-// Record layout of K1b / K1c.  Dense (cap == 0): chunk b's records start at
-// chunk_off[b], the exclusive scan of k_tok_count's counts.  Fixed capacity
-// (cap == kChunkCap): chunk b owns rec[b * cap, (b + 1) * cap) and pend
+// Record layout of K1b / K1c.  Dense (cap == 0): chunk c's records start at
+// chunk_off[c], the exclusive scan of k_tok_count's counts.  Fixed capacity
+// (cap == kChunkCap): chunk c owns rec[c * cap, (c + 1) * cap) and pend
 // likewise, no counting pass; K1b leaves the chunk's token count in
-// chunk_off[b] and the first sort pass gathers the used prefixes.
-// Inside its slot, chunk b's records start at a per-chunk rotation and wrap:
-// slots are 256 KiB apart and a Zipf chunk fills ~30 % of its slot, so
-// unrotated prefixes would all sit at the same low offsets of every slot and
-// load only the HBM channels those offsets interleave to.
+// chunk_off[c] and the first sort pass gathers the used prefixes.
+// Inside its slot, chunk c's records start at a per-chunk rotation and wrap:
+// a Zipf chunk fills ~30 % of its slot, so unrotated prefixes would all sit
+// at the same low offsets of every slot and load only the HBM channels those
+// offsets interleave to.
 constexpr uint64_t kChunkCap = kChunk / 2;  // a token start follows a whitespace byte
 static_assert((kChunkCap & (kChunkCap - 1)) == 0, "slot rotation wraps with a mask");
-__device__ __forceinline__ uint32_t chunk_rot(uint32_t b) {
-    return (uint32_t)(((b * 2654435761u) >> 22) << 5) & (uint32_t)(kChunkCap - 1);  // 256-B steps
+__device__ __forceinline__ uint32_t chunk_rot(uint64_t c) {
+    return (uint32_t)((((uint32_t)c * 2654435761u) >> 22) << 5) & (uint32_t)(kChunkCap - 1);  // 256-B steps
 }
-__device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap) {
-    return cap ? (uint64_t)blockIdx.x * cap : chunk_off[blockIdx.x];
+__device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap, uint64_t c) {
+    return cap ? c * cap : chunk_off[c];
 }
-// index of the chunk's j-th record (cbase from chunk_base, rot = chunk_rot(b))
+// index of the chunk's j-th record (cbase from chunk_base, rot = chunk_rot(c))
 __device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint64_t cap, uint32_t rot, uint32_t j) {
     return cap ? cbase + ((j + rot) & (uint32_t)(kChunkCap - 1)) : cbase + j;
 }
 
 // ---------------------------------------------------------------- K1b emit
-// A workgroup walks its 64 KiB chunk in rounds of 16 KiB: 4 windows of 16 B
-// per lane, window w = 256 j + lane, so each load instruction reads 1 KiB
-// contiguous.  Per round:
+// One wave per chunk (see "K1 chunks"), in rounds of kRound bytes: 2 windows
+// of 16 B per lane, window w = 64 j + lane, so each load instruction reads
+// 1 KiB contiguous; the next round is loaded while this one is worked on.
+// Per round, all in wave-private LDS:
 //   1. SWAR classes per window -> kept token starts (main.c:102-113) and the
-//      window's terminator / letter bit masks, kept in LDS;
-//   2. one block scan of 4 packed 16-bit counts -> the token index of every
-//      kept start in text order; the starts are listed in LDS;
-//   3. batches of 1024 tokens, 4 per thread, one token per lane: the register
-//      key path (masks + 12 bytes from LDS, 5-bit packing, main.c:105-111)
-//      and the hot-table home probe with 4 loads in flight per thread; a hit
+//      window's terminator / letter bit masks;
+//   2. one wave scan of 2 packed 16-bit counts -> the token index of every
+//      kept start in text order; the starts are listed;
+//   3. 64 tokens at a time, one per lane: the register key path (masks + 12
+//      bytes from LDS, 5-bit packing, main.c:105-111) and the hot-table
+//      probe (two lanes load the 32 B that begin a key's probe order); a hit
 //      stores its record straight to HBM (consecutive lanes, consecutive
-//      records);
-//   4. the batch's probe misses and general-path tokens (inner punctuation,
-//      > 12 letters, > 16 bytes) compacted in LDS, one per thread.
+//      records); probe misses and general-path tokens (inner punctuation,
+//      > 12 letters, > 16 bytes) are listed for K1c.
 // Records rec[i] = slot << 32 | file id0, in text order (the partial files'
 // "word id" lines, main.c:116).  First letters are counted per chunk
-// (chunk_hist = the partial_<letter>.txt line counts); tokens of > 12 letters
-// are queued for the hash-collision check.
-#ifndef II_K1_WIN
-#define II_K1_WIN 2  // 8 KiB rounds: half the LDS, 6 waves/SIMD (emit 14.5 -> 13.95 ms at 10 GB vs 16 KiB rounds)
-#endif
-#ifndef II_K1_MINWAVES
-#define II_K1_MINWAVES 6
-#endif
-constexpr int kWin = II_K1_WIN;                  // 16-B windows per lane per round
-constexpr int kRound = kWin * 16 * kBlock;       // 16 KiB of text per round
+// (chunk_hist = the partial_<letter>.txt line counts).
+constexpr int kWin = 2;                          // 16-B windows per lane per round
+constexpr int kRound = kWin * 16 * 64;           // 2 KiB of text per wave round
 constexpr int kRoundWins = kRound / 16;          // windows per round
-constexpr int kRoundStaged = kRound + kHalo;     // bytes staged in LDS after the left piece
+constexpr int kRoundHalo = 64;                   // bytes staged past the round (a fast key reads <= 16)
+constexpr int kHaloPieces = kRoundHalo / 16;
+constexpr int kRoundStaged = kRound + kRoundHalo;  // bytes staged in LDS after the left piece
 constexpr int kMaxRoundTok = kRound / 2;         // a token start needs a space before it
 static_assert(kChunk % kRound == 0, "a chunk is a whole number of rounds");
-static_assert(kWin * 16 <= 64, "4 packed 16-bit window counts per lane");
+static_assert(kWin * 16 <= 32, "2 packed 16-bit window counts per lane");
+
+// wave-private LDS of K1b
+struct EmitLds {
+    uint8_t text[16 + kRoundStaged];  // [0, 16): the 16 bytes before the round
+    uint32_t mask[kRoundWins + 1];    // per window: terminator (ws | NUL) bits | letter bits << 16
+    uint16_t off[kMaxRoundTok];       // round-local start of every kept token, text order
+};
 
 struct RoundRegs {
     uint4 v[kWin];  // lane's windows
-    uint4 h;        // left piece (lane 0) / halo pieces (lanes 1..32)
+    uint4 h;        // left piece (lane 0) / halo pieces (lanes 1..kHaloPieces)
 };
 __device__ __forceinline__ void fetch_round(RoundRegs& r, const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t lo) {
-    const int t = threadIdx.x;
+    const int l = lane_id();
 #pragma unroll
-    for (int j = 0; j < kWin; j++) r.v[j] = load16(text, nbytes, (int64_t)lo + 16 * (kBlock * j + t));
+    for (int j = 0; j < kWin; j++) r.v[j] = load16(text, nbytes, (int64_t)lo + 16 * (64 * j + l));
     r.h = make_uint4(0, 0, 0, 0);
-    if (t < kExtraPieces) r.h = load16(text, nbytes, (int64_t)lo + 16 * (t == 0 ? -1 : kRoundWins + t - 1));
+    if (l <= kHaloPieces) r.h = load16(text, nbytes, (int64_t)lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1));
 }
 __device__ __forceinline__ void store_round(uint8_t* s_text, const RoundRegs& r) {
-    const int t = threadIdx.x;
+    const int l = lane_id();
 #pragma unroll
-    for (int j = 0; j < kWin; j++) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (kBlock * j + t)) = r.v[j];
-    if (t < kExtraPieces) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (t == 0 ? -1 : kRoundWins + t - 1)) = r.h;
+    for (int j = 0; j < kWin; j++) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (64 * j + l)) = r.v[j];
+    if (l <= kHaloPieces) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (l == 0 ? -1 : kRoundWins + l - 1)) = r.h;
 }
 
 // 4 letters (bytes, first in the low byte) -> their 5-bit codes, first letter
@@ -633,87 +598,17 @@ __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint
     return true;
 }
 
-// Index of this lane's entry when the lanes with `want` append one entry each
-// to an LDS list: one LDS atomic per wave.  Call from wave-uniform control flow.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
-    const uint64_t m = __ballot(want);
-    if (m == 0) return 0;
-    const int leader = __builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    return base + (uint32_t)__popcll(m & lanemask_lt());
-}
-
-// Fast-path lookup of K1b from the match / occupied bit masks of the key's
-// 8-slot hot bucket: the slot holding the key; for a new word, the bucket's
-// first empty slot in probe order, claimed (table_find's rule, so a word
-// still lives in exactly one place); kSlotNone when the word takes the
-// resolve path (full bucket: the word is, or goes, in the big table; or the
-// claim raced).
-__device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t match, uint32_t full, uint64_t key,
-                                                   uint32_t home, uint64_t pos) {
-    const uint32_t h7 = home & (kBucket - 1);
-    const uint32_t bbase = home - h7;
-    if (match) return bbase + __builtin_ctz(match);
-    const uint32_t empty = ~full & 0xFFu;
-    if (!empty) return kSlotNone;
-    const uint32_t rot = ((empty >> h7) | (empty << (8 - h7))) & 0xFFu;
-    const uint32_t p = (h7 + __builtin_ctz(rot)) & (kBucket - 1);
-    return table_claim(t, bbase + p, key, pos) == key ? bbase + p : kSlotNone;
-}
-
-// 4 bits -> the even bits of a byte
-__device__ __forceinline__ uint32_t spread4(uint32_t x) {
-    x = (x | (x << 2)) & 0x33u;
-    return (x | (x << 1)) & 0x55u;
-}
-
-// Cooperative hot-bucket probe: every lane holds one token (key, home); the
-// wave probes its 64 tokens' buckets in 4 rounds of 16, 4 lanes per bucket
-// each loading one 16-B quarter, so a bucket costs one cache line access per
-// instruction (a lane-private 64-B probe would cost four).  probe_issue starts
-// the loads (unconditionally: a lane without a key probes the bucket of key 0,
-// harmlessly); probe_finish gives the owner lane its bucket's 8-bit match /
-// occupied masks.  Split so that a later token batch's loads can be in flight
-// while an earlier batch resolves.
+// Cooperative probe of the hot table: 32 tokens per load round, 2 rounds; a
+// lane pair loads the two 16-B slot pairs that begin the key's probe order in
+// its 8-slot bucket (home's pair and the next one), so one load instruction
+// touches one 64-B bucket per lane pair instead of four lines per lane.  A
+// frequent word sits at or next to its home slot (it was inserted while its
+// bucket was still empty), so the short window decides almost every token;
+// the rest go to K1c.  known = the slots seen.
 struct ProbeParts {
-    ulonglong2 q[4];
+    ulonglong2 q[2];
 };
 __device__ __forceinline__ void probe_issue(const Table& t, uint32_t home, ProbeParts& pp) {
-    const int l = lane_id();
-    const unsigned long long* base = t.keys + 2u * (l & 3);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const uint32_t h = (uint32_t)__shfl((int)home, 16 * r + (l >> 2), 64);
-        pp.q[r] = *reinterpret_cast<const ulonglong2*>(base + (h & ~(uint32_t)(kBucket - 1)));
-    }
-}
-__device__ __forceinline__ void probe_finish(uint64_t key, const ProbeParts& pp, uint32_t& match, uint32_t& full) {
-    const int l = lane_id();
-    match = full = 0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int src = 16 * r + (l >> 2);
-        const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), src, 64) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)key, src, 64);
-        const uint64_t m0 = __ballot(pp.q[r].x == k), m1 = __ballot(pp.q[r].y == k);
-        const uint64_t f0 = __ballot(pp.q[r].x != 0ull), f1 = __ballot(pp.q[r].y != 0ull);
-        if ((l >> 4) == r) {
-            const int b = 4 * (l & 15);
-            match = spread4((uint32_t)(m0 >> b) & 0xFu) | (spread4((uint32_t)(m1 >> b) & 0xFu) << 1);
-            full = spread4((uint32_t)(f0 >> b) & 0xFu) | (spread4((uint32_t)(f1 >> b) & 0xFu) << 1);
-        }
-    }
-}
-
-// Two-lane form (II_K1_PROBE == 2): 32 tokens per round, 2 rounds; a lane
-// pair loads the two 16-B slot pairs that begin the key's probe order
-// (home's pair and the next one), so a probe reads 32 B.  known = the slots
-// seen.  A frequent word sits at or next to its home slot (it was inserted
-// while its bucket was still empty), so the short window decides almost
-// every token; the rest go to K1c.
-__device__ __forceinline__ void probe_issue2(const Table& t, uint32_t home, ProbeParts& pp) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < 2; r++) {
@@ -722,8 +617,8 @@ __device__ __forceinline__ void probe_issue2(const Table& t, uint32_t home, Prob
         pp.q[r] = *reinterpret_cast<const ulonglong2*>(t.keys + (h & ~(uint32_t)(kBucket - 1)) + 2u * pair);
     }
 }
-__device__ __forceinline__ void probe_finish2(uint64_t key, uint32_t home, const ProbeParts& pp, uint32_t& match,
-                                              uint32_t& full, uint32_t& known) {
+__device__ __forceinline__ void probe_finish(uint64_t key, uint32_t home, const ProbeParts& pp, uint32_t& match,
+                                             uint32_t& full, uint32_t& known) {
     const int l = lane_id();
     const uint32_t p0 = (home & (kBucket - 1)) >> 1, p1 = (p0 + 1) & 3u;
     match = full = 0;
@@ -747,11 +642,12 @@ __device__ __forceinline__ void probe_finish2(uint64_t key, uint32_t home, const
     }
 }
 __device__ __forceinline__ uint32_t rotr8(uint32_t x, uint32_t s) { return ((x >> s) | (x << (8 - s))) & 0xFFu; }
-// bucket_resolve for a partly seen bucket: a match is the slot; otherwise the
-// first empty slot inside the seen prefix of the probe order is claimed; a
-// seen prefix with no empty slot leaves the word to K1c.
-__device__ __forceinline__ uint32_t bucket_resolve2(const Table& t, uint32_t match, uint32_t full, uint32_t known,
-                                                    uint64_t key, uint32_t home, uint64_t pos) {
+// Lookup from a partly seen bucket: a match is the slot; otherwise the first
+// empty slot inside the seen prefix of the probe order is claimed
+// (table_find's rule, so a word still lives in exactly one place); a seen
+// prefix with no empty slot, or a raced claim, leaves the word to K1c.
+__device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t match, uint32_t full, uint32_t known,
+                                                   uint64_t key, uint32_t home, uint64_t pos) {
     const uint32_t h7 = home & (kBucket - 1);
     const uint32_t bbase = home - h7;
     if (match) return bbase + __builtin_ctz(match);
@@ -763,262 +659,220 @@ __device__ __forceinline__ uint32_t bucket_resolve2(const Table& t, uint32_t mat
     return table_claim(t, bbase + p, key, pos) == key ? bbase + p : kSlotNone;
 }
 
-#ifndef II_K1_PROBE
-#define II_K1_PROBE 2
-#endif
-
 // Unresolved token of a chunk (K1b -> K1c), one u32: chunk-relative start
 // (16 bits) | chunk-relative token index << 16 (15 bits) | general path << 31.
 // A fast-path miss leaves its key in its record slot.
 constexpr uint32_t kPendSlow = 1u << 31;
-
-// Letter histogram update without same-address LDS atomics inside a wave:
-// lanes are matched on their 5-bit letter (5 ballots) and the lowest lane of
-// each group adds the group's size.  Call from wave-uniform control flow.
-__device__ __forceinline__ void wave_hist_add(uint32_t* hist, uint32_t letter, bool valid) {
-    uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 5; b++) {
-        const bool bit = (letter >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
-    }
-    if (valid && (m & lanemask_lt()) == 0) atomicAdd(&hist[letter], (uint32_t)__popcll(m));
-}
+static_assert(kChunk <= 65536 && kChunkCap <= 32768, "pending-token fields");
 
 // First-letter counts of the tokens one lane keys in a chunk: 8 bits per
-// letter in 7 registers (a lane keys at most kMaxRoundTok / kBlock = 32 tokens
-// per round, 128 per chunk), updated without LDS traffic; flushed once per
-// chunk as 14 wave sums of two 16-bit fields each.
+// letter in 7 registers (a lane keys at most kChunkCap / 64 = 128 tokens per
+// chunk), updated without LDS traffic.
 __device__ __forceinline__ void lane_hist_add(uint32_t (&lc)[7], uint32_t letter, bool valid) {
     const uint32_t inc = valid ? 1u << ((letter & 3u) * 8) : 0u;
     const uint32_t wi = letter >> 2;
 #pragma unroll
     for (int i = 0; i < 7; i++) lc[i] += wi == (uint32_t)i ? inc : 0u;
 }
-__device__ __forceinline__ void lane_hist_flush(const uint32_t (&lc)[7], uint32_t* hist) {
+static_assert(kChunkCap / 64 < 256, "8-bit per-lane letter counters");
+// The wave's letter counts: lane l < 26 receives letter l's (14 wave sums of
+// two 16-bit fields each).
+__device__ __forceinline__ uint32_t lane_hist_total(const uint32_t (&lc)[7]) {
+    const int l = lane_id();
+    uint32_t mine = 0;
 #pragma unroll
     for (int i = 0; i < 7; i++) {
 #pragma unroll
         for (int odd = 0; odd < 2; odd++) {
-            uint32_t v = (lc[i] >> (8 * odd)) & 0x00FF00FFu;  // letters 4i + odd, 4i + 2 + odd
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-            if (lane_id() == 0) {
-                const int l0 = 4 * i + odd, l1 = l0 + 2;
-                if (l0 < 26 && (v & 0xFFFFu)) atomicAdd(&hist[l0], v & 0xFFFFu);
-                if (l1 < 26 && (v >> 16)) atomicAdd(&hist[l1], v >> 16);
-            }
+            const uint32_t v = wave_sum32((lc[i] >> (8 * odd)) & 0x00FF00FFu);  // letters 4i + odd, 4i + 2 + odd
+            const int l0 = 4 * i + odd;
+            if (l == l0) mine = v & 0xFFFFu;
+            if (l == l0 + 2) mine = v >> 16;
         }
     }
+    return mine;
 }
 
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram.
 template <int kAblate = 0>
-__global__ __launch_bounds__(kBlock, II_K1_MINWAVES) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes,
+__global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                      const uint64_t* __restrict__ file_start,
-                                                     const uint32_t* __restrict__ file_id, uint32_t nfiles,
+                                                     const uint32_t* __restrict__ file_id,
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                      uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
                                                      const uint32_t* __restrict__ cf) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_text[16 + kRoundStaged];
-    __shared__ uint32_t s_mask[kRoundWins + 1];   // per window: terminator (ws | NUL) bits | letter bits << 16
-    __shared__ uint16_t s_off[kMaxRoundTok];      // round-local start of every kept token, text order
-    __shared__ uint64_t s_scan[kWaves + 1];
-    __shared__ uint32_t s_hist[32];
-    __shared__ uint32_t s_f[3];                   // first / last file of the chunk, id0 of the first
-    __shared__ uint32_t s_npend;
-
-    const int t = threadIdx.x;
-    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
+    __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
+    const uint64_t c = wave_chunk();
+    if (c >= nch) return;
+    EmitLds& W = s_lds[c - (uint64_t)blockIdx.x * kWG];
+    const int l = lane_id();
+    const uint64_t chunk_lo = c * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
-    if (t < 32) s_hist[t] = 0;
-    if (t < 3) s_f[t] = cf[3 * (uint64_t)blockIdx.x + t];  // k_chunk_files
-    if (t == 0) s_npend = 0;
-    const uint64_t cbase = chunk_base(chunk_off, cap);
-    const uint32_t rot = chunk_rot(blockIdx.x);
-    uint32_t out = 0;  // records emitted so far
+    // the chunk's files (k_chunk_files), wave-uniform
+    const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
+    const bool fsame = f_lo == f_hi;
+    const uint64_t cbase = chunk_base(chunk_off, cap, c);
+    const uint32_t rot = chunk_rot(c);
+    const uint64_t lt = lanemask_lt();
+    uint32_t out = 0;    // records emitted so far (wave-uniform)
+    uint32_t npend = 0;  // tokens left to K1c (wave-uniform)
     uint32_t lc[7] = {0, 0, 0, 0, 0, 0, 0};
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
     for (uint64_t lo = chunk_lo; lo < chunk_hi; lo += kRound) {
-        __syncthreads();  // the previous round's readers of s_text / s_off are done
-        store_round(s_text, nxt);
+        wave_sync();  // the previous round's readers of W are done
+        store_round(W.text, nxt);
         if (lo + kRound < chunk_hi) fetch_round(nxt, text, nbytes, lo + kRound);
-        __syncthreads();
+        wave_sync();
         // 1. kept starts and window masks (windows re-read from LDS: the next
-        //    round's bytes are already in flight in registers)
+        //    round's bytes are in flight in the registers)
         uint32_t kept[kWin];
-        uint64_t cnt = 0;
+        uint32_t cnt = 0;
 #pragma unroll
         for (int j = 0; j < kWin; j++) {
-            const uint32_t w = kBlock * j + t;
-            const uint4 v = *reinterpret_cast<const uint4*>(s_text + 16 + 16 * w);
+            const uint32_t w = 64 * j + l;
+            const uint4 v = *reinterpret_cast<const uint4*>(W.text + 16 + 16 * w);
             const Classes cl = classify16(v);
-            s_mask[w] = (cl.ws | cl.nul) | (cl.letter << 16);
-            const uint32_t prev = s_text[16 + 16 * w - 1];  // byte before the window
+            W.mask[w] = (cl.ws | cl.nul) | (cl.letter << 16);
+            const uint32_t prev = W.text[16 + 16 * w - 1];  // byte before the window
             const uint32_t starts = ~cl.ws & ((cl.ws << 1) | (is_ws(prev) ? 1u : 0u)) & 0xFFFFu;
-            kept[j] = kept_starts(starts, cl, s_text, text, nbytes, lo, 16 * w, kRoundStaged);
-            cnt |= (uint64_t)__popc(kept[j]) << (16 * j);
+            kept[j] = kept_starts(starts, cl, W.text, text, nbytes, lo, 16 * w, kRoundStaged);
+            cnt |= (uint32_t)__popc(kept[j]) << (16 * j);
         }
-        if (t == 0) {  // first halo window: masks past the round's last byte
-            const Classes ch = classify16(*reinterpret_cast<const uint4*>(s_text + 16 + kRound));
-            s_mask[kRoundWins] = (ch.ws | ch.nul) | (ch.letter << 16);
+        if (l == 0) {  // first halo window: masks past the round's last byte
+            const Classes ch = classify16(*reinterpret_cast<const uint4*>(W.text + 16 + kRound));
+            W.mask[kRoundWins] = (ch.ws | ch.nul) | (ch.letter << 16);
         }
         // 2. token index of every kept start (window j of all lanes before j + 1)
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan(cnt, &tot, s_scan);
-        uint32_t ntok = 0;
-#pragma unroll
-        for (int j = 0; j < kWin; j++) {
-            uint32_t o = ntok + (uint32_t)((ex >> (16 * j)) & 0xFFFFu);
-            const uint32_t wlo = 16 * (kBlock * j + t);
-            for (uint32_t m = kept[j]; m; m &= m - 1) s_off[o++] = (uint16_t)(wlo + __builtin_ctz(m));
-            ntok += (uint32_t)((tot >> (16 * j)) & 0xFFFFu);
+        const uint32_t inc = wave_incl_scan32(cnt);
+        const uint32_t ex = inc - cnt;
+        const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t ntok = (tot & 0xFFFFu) + (tot >> 16);
+        {
+            uint32_t o = ex & 0xFFFFu;
+            for (uint32_t m = kept[0]; m; m &= m - 1) W.off[o++] = (uint16_t)(16 * l + __builtin_ctz(m));
+            o = (tot & 0xFFFFu) + (ex >> 16);
+            for (uint32_t m = kept[1]; m; m &= m - 1) W.off[o++] = (uint16_t)(16 * (64 + l) + __builtin_ctz(m));
         }
-        __syncthreads();
-        const bool fsame = s_f[0] == s_f[1];
-        const uint32_t fid0 = s_f[2];
-        const uint32_t qbase = out, pbase = (uint32_t)(lo - chunk_lo);
-        // 3. keys + cooperative hot-bucket probes, one token per lane, no
-        //    barrier (two batches in flight per wave cost a wave per SIMD of
-        //    occupancy and measured slower)
-        struct Tok {
-            uint64_t key;
-            uint32_t p, home, first;
-            bool valid, fast;
-        };
-        auto tok_key = [&](Tok& k, uint32_t b0) {
-            const uint32_t q = b0 + t;
-            k.valid = q < ntok;
-            k.p = k.valid ? s_off[q] : 0u;
+        wave_sync();
+        const uint32_t pbase = (uint32_t)(lo - chunk_lo);
+        // 3. keys + cooperative hot-bucket probes, one token per lane
+        for (uint32_t b0 = 0; b0 < ntok; b0 += 64) {
+            const uint32_t q = b0 + l;
+            const bool valid = q < ntok;
+            const uint32_t p = valid ? W.off[q] : 0u;
             TokKey tk{0ull, 0u, 0u};
-            k.fast = k.valid && round_fast_key(s_text, s_mask, k.p, tk);
-            k.key = tk.key;
-            k.first = tk.first;
-            k.home = hot_slot(tk.key, tab.seed);
-            if (!(kAblate & 4)) lane_hist_add(lc, tk.first, k.fast);
-        };
-        auto tok_finish = [&](const Tok& k, const ProbeParts& pp, uint32_t b0) {
-            const uint32_t q = b0 + t;
+            const bool fast = valid && round_fast_key(W.text, W.mask, p, tk);
+            const uint32_t home = hot_slot(tk.key, tab.seed);
+            if (!(kAblate & 4)) lane_hist_add(lc, tk.first, fast);
             uint32_t slot = kSlotNone;
             if (kAblate & 1) {
-                if (k.fast) slot = k.home;
+                if (fast) slot = home;
             } else {
-                uint32_t match, full;
-#if II_K1_PROBE == 2
-                uint32_t known;
-                probe_finish2(k.key, k.home, pp, match, full, known);
-                if (k.fast) slot = bucket_resolve2(tab, match, full, known, k.key, k.home, lo + k.p);
-#else
-                probe_finish(k.key, pp, match, full);
-                if (k.fast) slot = bucket_resolve(tab, match, full, k.key, k.home, lo + k.p);
-#endif
+                ProbeParts pp;
+                probe_issue(tab, home, pp);  // all lanes: a lane without a key probes key 0's bucket, harmlessly
+                uint32_t match, full, known;
+                probe_finish(tk.key, home, pp, match, full, known);
+                if (fast) slot = bucket_resolve(tab, match, full, known, tk.key, home, lo + p);
             }
-            const bool resolved = k.fast && slot != kSlotNone;
+            const bool resolved = fast && slot != kSlotNone;
             const uint64_t ri = rec_slot(cbase, cap, rot, out + q);
             if (resolved) {
-                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, s_f[0], s_f[1], lo + k.p)];
+                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, lo + p)];
                 rec[ri] = ((uint64_t)slot << 32) | f;
-            } else if (k.fast) {
-                rec[ri] = k.key;
+            } else if (fast) {
+                rec[ri] = tk.key;
             }
-            const bool pending = k.valid && !resolved;
-            const uint32_t pi = wave_append(&s_npend, pending);
-            if (pending) pend[cbase + pi] = (pbase + k.p) | ((qbase + q) << 16) | (k.fast ? 0u : kPendSlow);
-        };
-        for (uint32_t b0 = 0; b0 < ntok; b0 += kBlock) {
-            Tok k;
-            ProbeParts pp;
-            tok_key(k, b0);
-#if II_K1_PROBE == 2
-            if (!(kAblate & 1)) probe_issue2(tab, k.home, pp);
-#else
-            if (!(kAblate & 1)) probe_issue(tab, k.home, pp);
-#endif
-            tok_finish(k, pp, b0);
+            const bool pending = valid && !resolved;
+            const uint64_t pm = __ballot(pending);
+            if (pending)
+                pend[cbase + npend + (uint32_t)__popcll(pm & lt)] =
+                    (pbase + p) | ((out + q) << 16) | (fast ? 0u : kPendSlow);
+            npend += (uint32_t)__popcll(pm);
         }
         out += ntok;
     }
-    lane_hist_flush(lc, s_hist);
-    __syncthreads();
-    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] = s_hist[t];
-    if (t == 0) {
-        pend_cnt[blockIdx.x] = s_npend;
-        if (cap) chunk_off[blockIdx.x] = out;  // fixed-capacity layout: the chunk's token count
+    const uint32_t h = lane_hist_total(lc);
+    if (l < 26) chunk_hist[c * 26 + l] = h;
+    if (l == 0) {
+        pend_cnt[c] = npend;
+        if (cap) chunk_off[c] = out;  // fixed-capacity layout: the chunk's token count
     }
 }
 
-// K1c: the tokens K1b left unresolved, one per thread across the chunk —
+// K1c: the tokens K1b left unresolved, one per lane, one wave per chunk —
 // general-path tokens (main.c:105-111 with inner punctuation, > 12 letters or
 // > 16 bytes: key from the text in HBM) and words whose hot bucket is full or
 // whose claim raced — full table lookup / insert (table_find), record.  Many
-// independent lookups in flight instead of a barrier-bound phase inside K1b.
-__global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restrict__ text, uint64_t nbytes,
+// independent lookups in flight instead of a phase inside K1b.  Tokens of
+// more than 12 letters (hashed keys) are queued for k_long_verify.
+__global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                         const uint64_t* __restrict__ file_start,
-                                                        const uint32_t* __restrict__ file_id, uint32_t nfiles,
+                                                        const uint32_t* __restrict__ file_id,
                                                         const uint64_t* __restrict__ chunk_off, uint64_t cap,
                                                         const uint32_t* __restrict__ pend,
                                                         const uint32_t* __restrict__ pend_cnt, Table tab,
                                                         uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                        LongTok* __restrict__ longs, uint64_t long_cap,
+                                                        LongTok* __restrict__ longs, uint64_t long_per,
                                                         const uint32_t* __restrict__ cf) {
-    __shared__ LongTok s_long[kLongBuf];
-    __shared__ uint32_t s_hist[32];
-    __shared__ uint32_t s_f[3];
-    __shared__ uint32_t s_lcount;
-    __shared__ uint64_t s_lbase;
-    const uint32_t n = pend_cnt[blockIdx.x];
+    __shared__ uint32_t s_hist[kWG][32];
+    const uint64_t c = wave_chunk();
+    if (c >= nch) return;
+    const uint32_t n = pend_cnt[c];
     if (n == 0) return;
-    const int t = threadIdx.x;
-    const uint64_t chunk_lo = (uint64_t)blockIdx.x * kChunk;
-    if (t < 32) s_hist[t] = 0;
-    if (t < 3) s_f[t] = cf[3 * (uint64_t)blockIdx.x + t];  // k_chunk_files
-    if (t == 0) s_lcount = 0;
-    __syncthreads();
-    const uint64_t cbase = chunk_base(chunk_off, cap);
-    const bool fsame = s_f[0] == s_f[1];
-    for (uint32_t i = t; i < n; i += kBlock) {
-        const uint32_t e = pend[cbase + i];
-        const uint64_t pos = chunk_lo + (e & 0xFFFFu);
-        const uint64_t r = rec_slot(cbase, cap, chunk_rot(blockIdx.x), (e >> 16) & 0x7FFFu);
-        uint64_t key;
-        uint32_t nlet = 0;
-        if (e & kPendSlow) {
-            const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
-            atomicAdd(&s_hist[k.first], 1u);
-            key = k.key;
-            nlet = k.nlet;
-        } else {
-            key = rec[r];
+    const int l = lane_id();
+    uint32_t* hist = s_hist[c - (uint64_t)blockIdx.x * kWG];
+    if (l < 32) hist[l] = 0;
+    wave_sync();
+    const uint64_t chunk_lo = c * kChunk;
+    const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
+    const bool fsame = f_lo == f_hi;
+    const uint64_t cbase = chunk_base(chunk_off, cap, c);
+    const uint32_t rot = chunk_rot(c);
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + l;
+        bool is_long = false;
+        uint64_t pos = 0, slot = 0;
+        if (i < n) {
+            const uint32_t e = pend[cbase + i];
+            pos = chunk_lo + (e & 0xFFFFu);
+            const uint64_t r = rec_slot(cbase, cap, rot, (e >> 16) & 0x7FFFu);
+            uint64_t key;
+            uint32_t nlet = 0;
+            if (e & kPendSlow) {
+                const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
+                atomicAdd(&hist[k.first], 1u);
+                key = k.key;
+                nlet = k.nlet;
+            } else {
+                key = rec[r];
+            }
+            slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
+            const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
+            rec[r] = (slot << 32) | f;
+            is_long = nlet > 12;
         }
-        const uint32_t slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-        const uint32_t f = fsame ? s_f[2] : file_id[file_of(file_start, s_f[0], s_f[1], pos)];
-        rec[r] = ((uint64_t)slot << 32) | f;
-        if (nlet > 12) {  // hashed key: queue for the exactness check
-            const uint32_t li = atomicAdd(&s_lcount, 1u);
-            if (li < (uint32_t)kLongBuf) {
-                s_long[li] = LongTok{pos, slot};
-            } else {  // the chunk alone overflows the buffer: straight to the global queue
-                const uint64_t g = atomicAdd((unsigned long long*)&tab.counters[C_LONG], 1ull);
-                if (g < long_cap) longs[g] = LongTok{pos, slot};
+        // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
+        const uint64_t lm = __ballot(is_long);
+        if (lm) {
+            const uint32_t shard = (uint32_t)(c & (kLongShards - 1));
+            const int leader = __builtin_ctzll(lm);
+            unsigned long long base = 0;
+            if (l == leader)
+                base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard], (unsigned long long)__popcll(lm));
+            base = (unsigned long long)__shfl((long long)base, leader, 64);
+            if (is_long) {
+                const uint64_t g = base + (uint64_t)__popcll(lm & lt);
+                if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
                 else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
             }
         }
     }
-    __syncthreads();
-    if (t < 26) chunk_hist[(uint64_t)blockIdx.x * 26 + t] += s_hist[t];
-    const uint32_t nl = s_lcount < (uint32_t)kLongBuf ? s_lcount : (uint32_t)kLongBuf;
-    if (nl) {
-        if (t == 0) s_lbase = atomicAdd((unsigned long long*)&tab.counters[C_LONG], (unsigned long long)nl);
-        __syncthreads();
-        for (uint32_t q = t; q < nl; q += kBlock) {
-            if (s_lbase + q < long_cap) longs[s_lbase + q] = s_long[q];
-            else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-        }
-    }
+    wave_sync();
+    if (l < 26 && hist[l]) chunk_hist[c * 26 + l] += hist[l];
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
@@ -1097,11 +951,14 @@ __device__ __forceinline__ int same_raw_token(const uint8_t* __restrict__ text, 
 // Exactness check for hashed keys: every long token must spell the same word
 // as its slot's representative occurrence.  Most occurrences repeat the
 // representative's bytes (same_raw_token); the rest are walked letter by letter.
+// Grid (kLongShards, y): blockIdx.x = the queue shard.
 __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                        const LongTok* __restrict__ longs, uint64_t nlong,
+                                                        const LongTok* __restrict__ longs, uint64_t long_per,
                                                         const uint64_t* __restrict__ rep, uint64_t* counters) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nlong; i += (uint64_t)gridDim.x * kBlock) {
-        LongTok lt = longs[i];
+    const uint64_t n = counters[C_LSHARD + 16 * blockIdx.x];
+    const LongTok* q = longs + blockIdx.x * long_per;
+    for (uint64_t i = (uint64_t)blockIdx.y * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.y * kBlock) {
+        LongTok lt = q[i];
         uint64_t a = lt.pos, b = rep[lt.slot];
         if (a == b || same_raw_token(text, nbytes, a, b)) continue;
         uint32_t na = 0, nb = 0;
@@ -1116,6 +973,24 @@ __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restric
         }
     }
 }
+
+// Totals of the long-token queue shards: counters[C_LONG] = all queued,
+// counters[C_LONGMAX] = the fullest shard.  One wave.
+__global__ void k_long_totals(uint64_t* counters) {
+    const uint64_t n = counters[C_LSHARD + 16 * lane_id()];
+    uint64_t m = n, t = n;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t x = (uint64_t)__shfl_xor((long long)m, o, 64);
+        m = x > m ? x : m;
+        t += (uint64_t)__shfl_xor((long long)t, o, 64);
+    }
+    if (lane_id() == 0) {
+        counters[C_LONG] = t;
+        counters[C_LONGMAX] = m;
+    }
+}
+static_assert(kLongShards == 64, "k_long_totals: one lane per shard");
 
 // Separator contract of ii_map_device: the byte before every file start is whitespace.
 __global__ void k_check_layout(const uint8_t* __restrict__ text, const uint64_t* __restrict__ file_start, uint32_t nfiles,

@@ -17,21 +17,23 @@ extern "C" int iigen_fill(const iigen_params*, const uint64_t*, uint8_t*, int);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 static float g_res;  // K1c time of the fastest emit run
-// read-only reference: the count kernel's access pattern (64 KiB per
-// workgroup, 16 B per lane, 8 loads in flight), XOR of the words
-__global__ __launch_bounds__(kBlock) void k_read_only(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t* out) {
-    const uint64_t lo = (uint64_t)blockIdx.x * kChunk;
+// read-only reference: the count kernel's access pattern (one wave per
+// chunk, 16 B per lane, 8 loads in flight), XOR of the words
+__global__ __launch_bounds__(kBlock) void k_read_only(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
+                                                      uint64_t* out) {
+    const uint64_t c = wave_chunk();
+    const uint64_t lo = c * kChunk;
     uint32_t x = 0;
-    if (lo + kChunk <= nbytes) {
-        for (int jb = 0; jb < 16; jb += 8) {
+    if (c < nch && lo + kChunk <= nbytes) {
+        for (int jb = 0; jb < (int)(kChunk / 1024); jb += 8) {
             uint4 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const uint4*>(text + lo + 16 * ((uint64_t)kBlock * (jb + u) + threadIdx.x));
+            for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const uint4*>(text + lo + 16 * (64ull * (jb + u) + lane_id()));
 #pragma unroll
             for (int u = 0; u < 8; u++) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
         }
     }
-    if (x == 0x12345678u) out[blockIdx.x] = x;
+    if (x == 0x12345678u) out[c] = x;
 }
 
 template <class F>
@@ -53,6 +55,7 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
     hipEvent_t a, b, c;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); CK(hipEventCreate(&c));
     uint32_t* cf;
+    const uint32_t wg = (uint32_t)((nch + kWG - 1) / kWG);
     CK(hipMalloc(&cf, 12 * nch));
     k_chunk_files<<<(uint32_t)((nch + kBlock - 1) / kBlock), kBlock>>>(fstart, fid, nf, nb, kChunk, nch, cf);
     float best = 1e9;
@@ -60,9 +63,9 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
         CK(hipMemset(tab.keys, 0, nslots * 8));
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
-        k_tok_emit<A><<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, tab, rec, chist, pend, pcnt, cf);
+        k_tok_emit<A><<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, tab, rec, chist, pend, pcnt, cf);
         CK(hipEventRecord(b));
-        k_tok_resolve<<<(uint32_t)nch, kBlock>>>(d_text, nb, fstart, fid, nf, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap, cf);
+        k_tok_resolve<<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap / kLongShards, cf);
         CK(hipEventRecord(c));
         CK(hipEventSynchronize(c));
         float ms, ms2; CK(hipEventElapsedTime(&ms, a, b)); CK(hipEventElapsedTime(&ms2, b, c));
@@ -92,7 +95,8 @@ int main(int argc, char** argv) {
     // count pass -> offsets (host scan)
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     CK(hipEventRecord(a));
-    k_tok_count<<<(uint32_t)nch, kBlock>>>(d_text, nb, chunk);
+    const uint32_t wg = (uint32_t)((nch + kWG - 1) / kWG);
+    k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms_count; CK(hipEventElapsedTime(&ms_count, a, b));
     std::vector<uint64_t> cnt(nch);
@@ -108,7 +112,7 @@ int main(int argc, char** argv) {
     printf("emit ablate %2d: %.3f ms  resolve %.3f ms\n", A, e_, g_res); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(0); RUN(1); RUN(4); RUN(5);
-    printf("count (best of 5): %.3f ms\n", best_of([&] { k_tok_count<<<(uint32_t)nch, kBlock>>>(d_text, nb, chunk); }));
-    printf("read-only (best of 5): %.3f ms\n", best_of([&] { k_read_only<<<(uint32_t)nch, kBlock>>>(d_text, nb, chunk); }));
+    printf("count (best of 5): %.3f ms\n", best_of([&] { k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
+    printf("read-only (best of 5): %.3f ms\n", best_of([&] { k_read_only<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
     return 0;
 }

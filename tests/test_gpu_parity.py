@@ -323,6 +323,21 @@ def test_logical_shards_balanced_letters(case, G):
     assert_same(shard_and_merge(text, off, G, balanced=True), expected, "%s G=%d balanced" % (case, G))
 
 
+def test_config5_shape_vs_oracle():
+    # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 files (far beyond the
+    # reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), ~3 KB files
+    nf = 100_000
+    t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
+    ids = list(range(nf))
+    exp = oracle_index(t, off, ids, threads=16)
+    with ii_ctypes.Index(0) as ix:
+        ix.map_host(t, off.tolist(), ids)
+        ix.reduce()
+        assert_same(ix.letters(), exp, "300 MB, 1e5 files, vocab 1e7")
+        st = ix.stats()
+    assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
+
+
 def test_large_vocab_vs_oracle_both_key_modes():
     # V ~ 2.2M distinct words (> 2^21): lexids need 22 bits, many words overflow
     # the hot level, so the word-id keys mix hot slots and big-table ranks;
