@@ -62,6 +62,9 @@ struct ii_ctx {
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
+    DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
+    uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
+    uint64_t lb_epoch = 0;       // epoch of the last onesweep pass
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
     uint64_t NW = 0;        // wid range
     // partial-file emitter (ii_partials)
@@ -248,35 +251,74 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     // as that allows (fewer buckets -> longer output runs per tile)
     const int npass = (hi - lo + kRadixBits - 1) / kRadixBits;
     const int bits = (hi - lo + npass - 1) / npass;
-    for (int shift = lo; shift < hi; shift += bits) {
+    // token sort: the passes after the first are onesweep passes (decoupled
+    // look-back) when their digits fit the histograms k_sort0_compact keeps
+    const bool sweep = remap0 && npass - 1 <= kLaterDigits;
+    uint64_t* dhist = nullptr;
+    if (sweep) {
+        CK(grow(c->dhist, sizeof(uint64_t) * 2 * kLaterDigits * kRadix));
+        dhist = P_<uint64_t>(c->dhist);
+        HIPCK(hipMemsetAsync(dhist, 0, sizeof(uint64_t) * kLaterDigits * kRadix, c->st));
+    }
+    for (int shift = lo, pass = 0; shift < hi; shift += bits, pass++) {
         const int db = std::min(bits, hi - shift);
         const uint32_t dmask = (1u << db) - 1u;
         const bool first0 = remap0 && shift == lo;
         const bool ev = timed && c->n_sc < kMaxTimedPasses;
+        const uint64_t* src = first0 ? *k2 : *k;
+        uint64_t* dst = first0 ? *k : *k2;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
             if (wid)
                 k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
                     *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept);
+                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist);
             else
                 k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
                     *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept);
+                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
+            if (sweep) k_digit_bases<<<kLaterDigits, kRadix, 0, c->st>>>(dhist, dhist + kLaterDigits * kRadix);
+        } else if (sweep) {
+            // onesweep: one launch per pass, no histogram pass, no table scan
+            const uint64_t ntiles = (n + kSweepTile - 1) / kSweepTile;
+            CK(grow(c->ticket, sizeof(uint32_t) * 4));
+            if (c->lb_cap < ntiles * kRadix) {
+                CK(grow(c->lbstat, sizeof(uint64_t) * ntiles * kRadix));
+                c->lb_cap = c->lbstat.cap / sizeof(uint64_t);
+                HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));  // epoch 0 = never published
+                c->lb_epoch = 0;
+            }
+            if (++c->lb_epoch >= (1u << 24)) {  // the 24-bit epoch wraps: clear once
+                HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));
+                c->lb_epoch = 1;
+            }
+            HIPCK(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->st));
+            if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
+            k_onesweep<kScatterThreads, kScatterItems><<<(uint32_t)ntiles, kScatterThreads, 0, c->st>>>(
+                src, dst, n, shift, db, dhist + kLaterDigits * kRadix + (uint64_t)(pass - 1) * kRadix,
+                P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch,
+                P_<unsigned long long>(c->counters) + C_OVERFLOW);
+            if (ev) {
+                HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
+                c->sc_bytes[c->n_sc] = 16 * n;
+                c->n_sc++;
+            }
+            HIPCK(hipGetLastError());
+            if (passes) (*passes)++;
+            std::swap(*k, *k2);
+            continue;
         } else {
             k_radix_hist<<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table);
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
         }
         if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        const uint64_t* src = first0 ? *k2 : *k;
-        uint64_t* dst = first0 ? *k : *k2;
         if (kv)
             k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, *v, *v2, n, chunk, shift, db,
                                                                       (uint32_t)nch, table, nullptr);
         else
-            k_radix_scatter<false, II_SC_NT, II_SC_IT><<<(uint32_t)nch, II_SC_NT, 0, c->st>>>(
+            k_radix_scatter<false, kScatterThreads, kScatterItems><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
                 src, dst, nullptr, nullptr, n, chunk, shift, db, (uint32_t)nch, table, first0 ? kept : nullptr);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
@@ -394,7 +436,8 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->okey2,    &c->oval,   &c->oval2, &c->P,       &c->loff,   &c->out,      &c->letter_off,
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
-                   &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend};
+                   &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
+                   &c->dhist,    &c->lbstat, &c->ticket};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -976,6 +1019,11 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
+    {
+        uint64_t ovf;
+        CK(read_u64(c, P_<uint64_t>(c->counters) + C_OVERFLOW, &ovf));
+        if (ovf & kLbTimeout) return II_ERR_INTERNAL;  // a onesweep look-back never resolved
+    }
 
     // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
     CK(run_unique(c, r, Tk, wid));

@@ -542,6 +542,7 @@ struct EmitLds {
     uint8_t text[16 + kRoundStaged];  // [0, 16): the 16 bytes before the round
     uint32_t mask[kRoundWins + 1];    // per window: terminator (ws | NUL) bits | letter bits << 16
     uint16_t off[kMaxRoundTok];       // round-local start of every kept token, text order
+    uint32_t hist[32];                // the chunk's first-letter counts
 };
 
 struct RoundRegs {
@@ -665,34 +666,6 @@ __device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t matc
 constexpr uint32_t kPendSlow = 1u << 31;
 static_assert(kChunk <= 65536 && kChunkCap <= 32768, "pending-token fields");
 
-// First-letter counts of the tokens one lane keys in a chunk: 8 bits per
-// letter in 7 registers (a lane keys at most kChunkCap / 64 = 128 tokens per
-// chunk), updated without LDS traffic.
-__device__ __forceinline__ void lane_hist_add(uint32_t (&lc)[7], uint32_t letter, bool valid) {
-    const uint32_t inc = valid ? 1u << ((letter & 3u) * 8) : 0u;
-    const uint32_t wi = letter >> 2;
-#pragma unroll
-    for (int i = 0; i < 7; i++) lc[i] += wi == (uint32_t)i ? inc : 0u;
-}
-static_assert(kChunkCap / 64 < 256, "8-bit per-lane letter counters");
-// The wave's letter counts: lane l < 26 receives letter l's (14 wave sums of
-// two 16-bit fields each).
-__device__ __forceinline__ uint32_t lane_hist_total(const uint32_t (&lc)[7]) {
-    const int l = lane_id();
-    uint32_t mine = 0;
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-#pragma unroll
-        for (int odd = 0; odd < 2; odd++) {
-            const uint32_t v = wave_sum32((lc[i] >> (8 * odd)) & 0x00FF00FFu);  // letters 4i + odd, 4i + 2 + odd
-            const int l0 = 4 * i + odd;
-            if (l == l0) mine = v & 0xFFFFu;
-            if (l == l0 + 2) mine = v >> 16;
-        }
-    }
-    return mine;
-}
-
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram.
 template <int kAblate = 0>
@@ -718,7 +691,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     const uint64_t lt = lanemask_lt();
     uint32_t out = 0;    // records emitted so far (wave-uniform)
     uint32_t npend = 0;  // tokens left to K1c (wave-uniform)
-    uint32_t lc[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (l < 32) W.hist[l] = 0;
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
     for (uint64_t lo = chunk_lo; lo < chunk_hi; lo += kRound) {
@@ -766,7 +739,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             TokKey tk{0ull, 0u, 0u};
             const bool fast = valid && round_fast_key(W.text, W.mask, p, tk);
             const uint32_t home = hot_slot(tk.key, tab.seed);
-            if (!(kAblate & 4)) lane_hist_add(lc, tk.first, fast);
+            if (!(kAblate & 4) && fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS; same-letter lanes serialize in the LDS unit, not in VALU
             uint32_t slot = kSlotNone;
             if (kAblate & 1) {
                 if (fast) slot = home;
@@ -794,8 +767,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
         }
         out += ntok;
     }
-    const uint32_t h = lane_hist_total(lc);
-    if (l < 26) chunk_hist[c * 26 + l] = h;
+    wave_sync();
+    if (l < 26) chunk_hist[c * 26 + l] = W.hist[l];
     if (l == 0) {
         pend_cnt[c] = npend;
         if (cap) chunk_off[c] = out;  // fixed-capacity layout: the chunk's token count
@@ -1204,32 +1177,19 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // layout or at i in the dense one (cap == 0).  Its kept records go to
 // kout[voff[c0] ...): kept[b] = their number, kept[kMaxChunks + b] =
 // voff[c0], the range pass 0's scatter reads back.
-// the dedup bitmap covers the first 2^II_DEDUP_LOG2 hot slots (1 bit each in
-// LDS); hot words beyond it are not deduplicated here (measured: covering
-// only half of a 2^20-slot hot level doubled the sort time)
-#ifndef II_DEDUP_LOG2
-#define II_DEDUP_LOG2 20  // the whole hot level: a 128 KiB bitmap, one 1024-thread workgroup per CU
-#endif
-constexpr uint64_t kDedupSlots = kHotSlots < (1ull << II_DEDUP_LOG2) ? kHotSlots : (1ull << II_DEDUP_LOG2);
-constexpr uint32_t kDedupWords = (uint32_t)(kDedupSlots / 32);
-#ifndef II_S0_DEFER
-#define II_S0_DEFER 0  // 1: a tile's kept records are stored one tile later (gathers overlap the next loads)
-#endif
-#ifndef II_S0_TTS
-#define II_S0_TTS 0
-#endif
-#ifndef II_S0_NT
-#define II_S0_NT 1024
-#endif
-#ifndef II_S0_IT
-#define II_S0_IT 8
-#endif
-constexpr int kCBlock = II_S0_NT;               // 16 waves share one 128 KiB dedup bitmap
-constexpr int kS0Items = II_S0_IT;              // records per thread per tile
+// The dedup bitmap covers the whole hot level (1 bit per slot in LDS, 128
+// KiB: one 1024-thread workgroup per CU; covering only half of it doubled
+// the sort time).  The kept records' later radix digits are counted here too
+// (dhist, global atomics per workgroup): the onesweep passes that follow need
+// only those global counts, not a per-tile histogram pass.
+constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
+constexpr int kCBlock = 1024;                   // 16 waves share one 128 KiB dedup bitmap
+constexpr int kS0Items = 8;                     // records per thread per tile
 constexpr int kCWaves = kCBlock / 64;
-constexpr int kCTile = kS0Items * kCBlock;    // records per tile
+constexpr int kCTile = kS0Items * kCBlock;      // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
-// LDS: 16 KiB counts + 128 KiB bitmap + 4 KiB offsets: one workgroup (16 waves) per CU
+constexpr int kLaterDigits = 2;                 // digits counted for the onesweep passes
+// LDS: 16 KiB counts + 128 KiB bitmap + 4 KiB offsets + 2 KiB later digits: one workgroup per CU
 
 template <bool kWid>
 __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
@@ -1237,15 +1197,18 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
                                                            uint32_t nchunks, uint64_t* __restrict__ table,
                                                            const uint32_t* __restrict__ remap,
-                                                           uint64_t* __restrict__ kout, uint64_t* __restrict__ kept) {
+                                                           uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
+                                                           int shift1, int shift2, uint64_t* __restrict__ dhist) {
     __shared__ uint32_t cnt[kCWaves][kRadix];
     __shared__ uint32_t bm[kDedupWords];
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
+    __shared__ uint32_t s_later[kLaterDigits][kRadix];
     __shared__ uint32_t s_wtot[kCWaves];
     __shared__ uint32_t s_epoch, s_flag;
     const int w = wave_id(), l = lane_id();
     const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
     for (int i = threadIdx.x; i < kCWaves * kRadix; i += kCBlock) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += kCBlock) (&s_later[0][0])[i] = 0;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
     for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
     if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
@@ -1259,10 +1222,10 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
     uint64_t o = lo;  // next output position
-    // (prefetching the next tile, before or after the remap gathers, measured
-    // slower: 5.3 -> 5.9-6.2 ms at 10 GB)
-    uint64_t nraw[kS0Items];
-    auto load_tile = [&](uint64_t tb) {
+    // (prefetching the next tile, deferring the stores by one tile, and
+    // test-before-set in the bitmap all measured no faster)
+    for (uint64_t tb = lo; tb < hi; tb += kCTile) {
+        uint64_t raw[kS0Items];
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
@@ -1280,34 +1243,8 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                 }
                 src = gbase + ((ri + gadj) & (uint32_t)(kChunkCap - 1));
             }
-            nraw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
+            raw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
         }
-    };
-#if II_S0_DEFER
-    uint32_t p_fid[kS0Items], p_lex[kS0Items], p_pos[kS0Items];
-    uint32_t p_keep = 0;
-    uint64_t p_base = 0;
-    auto st_prev = [&]() {
-#pragma unroll
-        for (int k = 0; k < kS0Items; k++) {
-            if ((p_keep >> k) & 1u) {
-                const uint64_t r = ((uint64_t)p_lex[k] << 32) | p_fid[k];
-                st_nt(kout + p_base + p_pos[k], r);
-                atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
-            }
-        }
-    };
-#endif
-    for (uint64_t tb = lo; tb < hi; tb += kCTile) {
-        load_tile(tb);
-#if II_S0_DEFER
-        // store the previous tile while this tile's loads are in flight: its
-        // remap gathers were issued one tile ago
-        st_prev();
-#endif
-        uint64_t raw[kS0Items];
-#pragma unroll
-        for (int k = 0; k < kS0Items; k++) raw[k] = nraw[k];
         if (threadIdx.x == 0) {  // thread 0's item 0 is the tile's first record
             const uint32_t f = (uint32_t)raw[0];
             s_flag = f != s_epoch;
@@ -1320,58 +1257,23 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         }
         const uint32_t epoch = s_epoch;
         uint32_t keep = 0, wcount = 0;
-#if II_S0_DEFER
-        uint32_t (&pos)[kS0Items] = p_pos;  // the previous tile's positions are consumed by now
-#else
         uint32_t pos[kS0Items];
-#endif
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
-            if (ok && slot < kDedupSlots && (uint32_t)raw[k] == epoch) {
+            if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
                 const uint32_t bit = 1u << (slot & 31);
-#if II_S0_TTS
-                // test before set: a slot already seen in this epoch is dropped
-                // with a plain LDS read; only first sightings pay the atomic
-                ok = !(bm[slot >> 5] & bit) && !(atomicOr(&bm[slot >> 5], bit) & bit);
-#else
                 ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
-#endif
             }
             const uint64_t b = __ballot(ok);
             pos[k] = wcount + (uint32_t)__popcll(b & lt);
             wcount += (uint32_t)__popcll(b);
             keep |= (uint32_t)ok << k;
         }
-#if II_S0_DEFER
-#pragma unroll
-        for (int k = 0; k < kS0Items; k++) {  // this tile's gathers, consumed one tile later
-            p_fid[k] = (uint32_t)raw[k];
-            p_lex[k] = ((keep >> k) & 1u) ? ((kWid && (raw[k] >> 32) < kHotSlots) ? (uint32_t)(raw[k] >> 32)
-                                                                                   : remap[raw[k] >> 32])
-                                          : 0u;
-        }
-        p_keep = keep;
-        if (l == 0) s_wtot[w] = wcount;
-        __syncthreads();
-        uint32_t wbase = 0, ttot = 0;
-#pragma unroll
-        for (int ww = 0; ww < kCWaves; ww++) {
-            const uint32_t c = s_wtot[ww];
-            if (ww < w) wbase += c;
-            ttot += c;
-        }
-        p_base = o + wbase;
-        o += ttot;
-        __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
-    }
-    st_prev();  // the last tile
-    __syncthreads();
-#else
         // the remap gathers of the kept records are in flight across the barrier
 #pragma unroll
-        for (int k = 0; k < kS0Items; k++)  // slot -> lexicographic id, in place
+        for (int k = 0; k < kS0Items; k++)  // slot -> sort key, in place
             if ((keep >> k) & 1u) {
                 const uint32_t slot = (uint32_t)(raw[k] >> 32);
                 // wid keys: only big-table words need the map (remap = wmap)
@@ -1393,17 +1295,24 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                 const uint64_t r = raw[k];
                 st_nt(kout + o + wbase + pos[k], r);
                 atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
+                if (dhist) {
+                    atomicAdd(&s_later[0][(uint32_t)(r >> shift1) & dmask], 1u);
+                    atomicAdd(&s_later[1][(uint32_t)(r >> shift2) & dmask], 1u);
+                }
             }
         }
         o += ttot;
         __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
     }
-#endif
     for (int d = threadIdx.x; d < kRadix; d += kCBlock) {
         uint32_t tt = 0;
 #pragma unroll
         for (int ww = 0; ww < kCWaves; ww++) tt += cnt[ww][d];
         table[(uint64_t)d * nchunks + blockIdx.x] = tt;
+        if (dhist) {
+            if (s_later[0][d]) atomicAdd((unsigned long long*)&dhist[d], (unsigned long long)s_later[0][d]);
+            if (s_later[1][d]) atomicAdd((unsigned long long*)&dhist[kRadix + d], (unsigned long long)s_later[1][d]);
+        }
     }
     if (threadIdx.x == 0) {
         kept[blockIdx.x] = o - lo;

@@ -161,18 +161,10 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortItems = 16;                     // keys per thread per tile
 constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
-#ifndef II_SC_NT
-#define II_SC_NT 512  // threads per workgroup of the token-sort scatter (tile = II_SC_NT * II_SC_IT keys; 512 x 16 measured best: 1.95 ms vs 2.22 for 256, 2.39 for 1024, 2.66 for 512 x 24 at 10 GB)
-#endif
-#ifndef II_SC_IT
-#define II_SC_IT 16  // keys per thread per tile of the token-sort scatter
-#endif
-#ifndef II_HIST_V2
-#define II_HIST_V2 1  // k_radix_hist reads two keys per 16-B load
-#endif
-#ifndef II_SC_PF
-#define II_SC_PF 0  // 1: the scatter issues the next tile's loads before ranking this one
-#endif
+constexpr int kScatterThreads = 512;              // token-sort scatter: tiles of 512 x 16 keys (runs twice as long
+constexpr int kScatterItems = 16;                  // as 256 x 16: 2.22 -> 1.95 ms per pass at 10 GB; 1024 x 16 and
+                                                   // 512 x 24 were slower)
+constexpr int kSweepTile = kScatterThreads * kScatterItems;  // keys per onesweep tile
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).  Same
@@ -185,11 +177,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint32_t* mine = cnt[wave_id()];
-    const uint64_t tofs = (uint64_t)wave_id() * 64 * kSortItems + lane_id();
-#if II_HIST_V2
     // the histogram ignores order: 16-B loads (two keys per lane, 1 KiB per
     // wave instruction); lo and the tile are even, so a pair is split only at hi
-    (void)tofs;
     const uint64_t pofs = (uint64_t)wave_id() * 64 * kSortItems + 2 * (uint64_t)lane_id();
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
         ulonglong2 raw[kSortItems / 2];
@@ -208,19 +197,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
             if (idx + 1 < hi) atomicAdd(&mine[(uint32_t)(raw[k].y >> shift) & dmask], 1u);
         }
     }
-#else
-    for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
-        uint64_t raw[kSortItems];
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
-            const uint64_t idx = tb + tofs + (uint64_t)k * 64;
-            raw[k] = idx < hi ? ld_nt(keys + idx) : 0ull;
-        }
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++)
-            if (tb + tofs + (uint64_t)k * 64 < hi) atomicAdd(&mine[(uint32_t)(raw[k] >> shift) & dmask], 1u);
-    }
-#endif
     __syncthreads();
     for (int d = threadIdx.x; d < kRadix; d += kBlock) {
         uint32_t t = 0;
@@ -295,9 +271,6 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
             key[k] = nkey[k];
             if (kHasVals) val[k] = nval[k];
         }
-#if II_SC_PF
-        if (tb + kTileN < hi) load_tile(tb + kTileN);
-#endif
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < IT; k++) {
@@ -361,9 +334,7 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
             }
         }
         __syncthreads();
-#if !II_SC_PF
-        if (tb + kTileN < hi) load_tile(tb + kTileN);
-#endif
+        if (tb + kTileN < hi) load_tile(tb + kTileN);  // (issuing them before the ranking measured slower)
         const uint32_t tile_n = (uint32_t)all;
 #pragma unroll
         for (int j = 0; j < IT; j++) {
@@ -380,6 +351,175 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
         if (digit_thread) s_run[t] += tot_d;
         // the next iteration's first __syncthreads orders this update before use
     }
+}
+
+// ----------------------------------------------------------------------------
+// Onesweep scatter pass (decoupled look-back, no histogram pass): the global
+// count of every digit is known up front (dbase[d] = exclusive prefix over
+// digits, counted while an earlier pass wrote the keys), so a tile only needs
+// the number of keys with digit d in all EARLIER tiles.  Tiles are claimed in
+// order from a ticket counter (a tile waits only on tiles whose workgroups
+// are already running: no deadlock whatever the residency); each tile
+// publishes, per digit, its own count (flag A), looks back over earlier
+// tiles' entries — summing A counts until it meets an inclusive prefix
+// (flag P) — and publishes its inclusive prefix (P).  Every entry is one
+// naturally aligned 8-byte granule written by one agent-scope store and read
+// by agent-scope loads (cross-XCD visible without fences,
+// MI355X_MICROARCH.md "inter-workgroup visibility"):
+//   bits 63..40 epoch of the pass (entries of other passes read as "not
+//   yet"; no clearing between passes), 39..38 flag, 37..0 count.
+// Same tile shape, ranking and store runs as k_radix_scatter.
+constexpr uint64_t kLbFlagA = 1ull << 38, kLbFlagP = 2ull << 38, kLbValMask = (1ull << 38) - 1;
+constexpr unsigned long long kLbTimeout = 8;  // error bit (counters[C_OVERFLOW]) of a look-back that never resolved
+template <int NT, int IT>
+__global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                 uint64_t n, int shift, int dbits, const uint64_t* __restrict__ dbase,
+                                                 uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
+                                                 uint64_t epoch, unsigned long long* __restrict__ err) {
+    constexpr int NW = NT / 64;
+    constexpr int kTileN = NT * IT;
+    constexpr int kDW = kRadix / 64;
+    static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
+    __shared__ uint64_t s_keys[kTileN];
+    __shared__ uint32_t s_wcnt[NW][kRadix];
+    __shared__ uint32_t s_tstart[kRadix];
+    __shared__ uint64_t s_run[kRadix];
+    __shared__ uint64_t s_scan[kDW];
+    __shared__ uint32_t s_tile;
+
+    const int w = wave_id(), l = lane_id(), t = threadIdx.x;
+    const uint32_t ndig = 1u << dbits, dmask = ndig - 1u;
+    const bool digit_thread = t < (int)ndig;
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+    if (t < kRadix) {
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) s_wcnt[ww][t] = 0;
+    }
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const uint64_t tb = tile * kTileN;
+    const uint64_t lt = lanemask_lt();
+    const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
+    uint64_t key[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const uint64_t idx = wbase + (uint64_t)k * 64;
+        key[k] = idx < n ? kin[idx] : ~0ull;
+    }
+    uint32_t rank[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const bool valid = wbase + (uint64_t)k * 64 < n;
+        const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; b++) {
+            if (b < dbits) {
+                const bool bit = (d >> b) & 1;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+        }
+        uint32_t r = 0;
+        if (valid) {
+            const uint32_t before = s_wcnt[w][d];
+            r = before + __popcll(m & lt);
+            if ((m & lt) == 0) s_wcnt[w][d] = before + __popcll(m);
+        }
+        rank[k] = r;
+    }
+    __syncthreads();
+    uint32_t cw[NW];
+    uint32_t tot_d = 0;
+    if (t < kRadix) {
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            cw[ww] = s_wcnt[ww][t];
+            tot_d += cw[ww];
+        }
+    }
+    // look-back: publish this tile's count, sum the earlier tiles' counts
+    if (digit_thread) {
+        uint64_t* mine = status + tile * kRadix + t;
+        const uint64_t ep = epoch << 40;
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(mine, ep | kLbFlagP | tot_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(mine, ep | kLbFlagA | tot_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint64_t p = tile; p-- > 0;) {
+                const uint64_t* e = status + p * kRadix + t;
+                uint64_t v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // tile p has not published yet (its workgroup is running); a wait of seconds means a
+                // broken hand-off: flag it and let the launch drain rather than spin forever
+                for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {
+                    if (spin == (1u << 24)) {
+                        atomicOr(err, kLbTimeout);
+                        v = epoch << 40 | kLbFlagP;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                excl += v & kLbValMask;
+                if (v & kLbFlagP) break;
+            }
+            __hip_atomic_store(mine, ep | kLbFlagP | (excl + tot_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_run[t] = dbase[t] + excl;
+    }
+    // digit t: tile start, per-wave offsets (as k_radix_scatter)
+    const uint64_t inc = wave_incl_scan(tot_d);
+    if (w < kDW && l == 63) s_scan[w] = inc;
+    __syncthreads();
+    uint64_t wb = 0, all = 0;
+#pragma unroll
+    for (int ww = 0; ww < kDW; ww++) {
+        const uint64_t sv = s_scan[ww];
+        if (ww < w) wb += sv;
+        all += sv;
+    }
+    if (t < kRadix) {
+        uint32_t run = (uint32_t)(wb + inc - tot_d);
+        s_tstart[t] = run;
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            s_wcnt[ww][t] = run;
+            run += cw[ww];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        if (wbase + (uint64_t)k * 64 < n) {
+            const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
+            s_keys[s_wcnt[w][d] + rank[k]] = key[k];
+        }
+    }
+    __syncthreads();
+    const uint32_t tile_n = (uint32_t)all;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        const uint32_t p = j * NT + t;
+        if (p < tile_n) {
+            const uint64_t k = s_keys[p];
+            const uint32_t d = (uint32_t)(k >> shift) & dmask;
+            kout[s_run[d] + (p - s_tstart[d])] = k;
+        }
+    }
+}
+
+// dbase[r * kRadix + d] = exclusive prefix over digits of dhist[r * kRadix + d]
+// (one workgroup per row).
+__global__ __launch_bounds__(kRadix) void k_digit_bases(const uint64_t* __restrict__ dhist, uint64_t* __restrict__ dbase) {
+    __shared__ uint64_t lds[kRadix / 64 + 1];
+    const uint64_t v = dhist[blockIdx.x * kRadix + threadIdx.x];
+    const uint64_t inc = wave_incl_scan(v);
+    if (lane_id() == 63) lds[wave_id()] = inc;
+    __syncthreads();
+    uint64_t base = 0;
+    for (int w = 0; w < wave_id(); w++) base += lds[w];
+    dbase[blockIdx.x * kRadix + threadIdx.x] = base + inc - v;
 }
 
 }  // namespace ii
