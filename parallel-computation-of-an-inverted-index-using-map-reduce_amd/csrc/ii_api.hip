@@ -296,7 +296,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             }
             HIPCK(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->st));
             if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-            k_onesweep<kScatterThreads, kScatterItems><<<(uint32_t)ntiles, kScatterThreads, 0, c->st>>>(
+            k_onesweep<kSweepThreads, kSweepItems><<<(uint32_t)ntiles, kSweepThreads, 0, c->st>>>(
                 src, dst, n, shift, db, dhist + kLaterDigits * kRadix + (uint64_t)(pass - 1) * kRadix,
                 P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch,
                 P_<unsigned long long>(c->counters) + C_OVERFLOW);

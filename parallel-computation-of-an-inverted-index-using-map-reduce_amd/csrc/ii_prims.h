@@ -164,7 +164,14 @@ constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
 constexpr int kScatterThreads = 512;              // token-sort scatter: tiles of 512 x 16 keys (runs twice as long
 constexpr int kScatterItems = 16;                  // as 256 x 16: 2.22 -> 1.95 ms per pass at 10 GB; 1024 x 16 and
                                                    // 512 x 24 were slower)
-constexpr int kSweepTile = kScatterThreads * kScatterItems;  // keys per onesweep tile
+#ifndef II_SWEEP_NT
+#define II_SWEEP_NT 512
+#endif
+#ifndef II_SWEEP_IT
+#define II_SWEEP_IT 16
+#endif
+constexpr int kSweepThreads = II_SWEEP_NT, kSweepItems = II_SWEEP_IT;
+constexpr int kSweepTile = kSweepThreads * kSweepItems;  // keys per onesweep tile
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).  Same
@@ -385,6 +392,7 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
     __shared__ uint32_t s_tstart[kRadix];
     __shared__ uint64_t s_run[kRadix];
     __shared__ uint64_t s_scan[kDW];
+    __shared__ uint32_t s_tot[kRadix];
     __shared__ uint32_t s_tile;
 
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
@@ -438,35 +446,53 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
             tot_d += cw[ww];
         }
     }
-    // look-back: publish this tile's count, sum the earlier tiles' counts
+    // look-back: publish this tile's count at once, then sum the earlier
+    // tiles' counts — four lanes per digit, each loading the entry of a
+    // different earlier tile, so a chain of A entries is walked four tiles per
+    // round trip
+    const uint64_t ep = epoch << 40;
     if (digit_thread) {
-        uint64_t* mine = status + tile * kRadix + t;
-        const uint64_t ep = epoch << 40;
+        s_tot[t] = tot_d;
+        __hip_atomic_store(status + tile * kRadix + t, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | tot_d,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint32_t gj = t & 3;  // place of this lane in its quad
+    for (uint32_t gd = t >> 2; gd < ndig; gd += NT / 4) {  // the quad's digit; control flow is quad-uniform
         uint64_t excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(mine, ep | kLbFlagP | tot_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(mine, ep | kLbFlagA | tot_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint64_t p = tile; p-- > 0;) {
-                const uint64_t* e = status + p * kRadix + t;
-                uint64_t v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t base = (int64_t)tile - 1; base >= 0; base -= 4) {
+            const int64_t p = base - (int64_t)gj;
+            uint64_t v = kLbFlagP;  // before tile 0: an inclusive prefix of 0
+            if (p >= 0) {
+                const uint64_t* e = status + (uint64_t)p * kRadix + gd;
+                v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // tile p has not published yet (its workgroup is running); a wait of seconds means a
                 // broken hand-off: flag it and let the launch drain rather than spin forever
                 for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {
                     if (spin == (1u << 24)) {
                         atomicOr(err, kLbTimeout);
-                        v = epoch << 40 | kLbFlagP;
+                        v = ep | kLbFlagP;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
                     v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                excl += v & kLbValMask;
-                if (v & kLbFlagP) break;
             }
-            __hip_atomic_store(mine, ep | kLbFlagP | (excl + tot_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the nearest inclusive prefix among the quad's four tiles ends the walk
+            const uint32_t q = (uint32_t)(__ballot((v & kLbFlagP) != 0) >> (lane_id() & ~3)) & 0xFu;
+            const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 3u;
+            uint64_t add = gj <= upto ? (v & kLbValMask) : 0;
+            add += (uint64_t)__shfl_xor((long long)add, 1, 64);
+            add += (uint64_t)__shfl_xor((long long)add, 2, 64);
+            excl += add;
+            if (q) break;
         }
-        s_run[t] = dbase[t] + excl;
+        if (gj == 0) {
+            if (tile != 0)
+                __hip_atomic_store(status + tile * kRadix + gd, ep | kLbFlagP | (excl + s_tot[gd]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_run[gd] = dbase[gd] + excl;
+        }
     }
     // digit t: tile start, per-wave offsets (as k_radix_scatter)
     const uint64_t inc = wave_incl_scan(tot_d);
