@@ -199,9 +199,10 @@ static int run_reduce(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
     return II_OK;
 }
 
-struct OpU32 {
+// pending tokens of a chunk: two 16-bit counts (k_tok_emit)
+struct OpPendCount {
     const uint32_t* a;
-    __device__ uint64_t value(uint64_t i) const { return a[i]; }
+    __device__ uint64_t value(uint64_t i) const { return (a[i] & 0xFFFFu) + (a[i] >> 16); }
     __device__ void emit(uint64_t, uint64_t, uint64_t) const {}
 };
 
@@ -210,6 +211,26 @@ struct OpInPlace {
     __device__ uint64_t value(uint64_t i) const { return a[i]; }
     __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { a[i] = ex; }
 };
+
+// Look-back state for one decoupled-look-back launch with `entries` 8-byte
+// granules: a new epoch (entries of earlier launches then read as "not yet
+// published", so nothing is cleared between launches; cleared once when the
+// buffer grows or the 24-bit epoch wraps) and a zeroed tile ticket.
+static int lookback_pass(ii_ctx* c, uint64_t entries) {
+    CK(grow(c->ticket, sizeof(uint32_t) * 4));
+    if (c->lb_cap < entries) {
+        CK(grow(c->lbstat, sizeof(uint64_t) * entries));
+        c->lb_cap = c->lbstat.cap / sizeof(uint64_t);
+        HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));  // epoch 0 = never published
+        c->lb_epoch = 0;
+    }
+    if (++c->lb_epoch >= (1u << 24)) {
+        HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));
+        c->lb_epoch = 1;
+    }
+    HIPCK(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->st));
+    return II_OK;
+}
 
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
@@ -283,18 +304,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         } else if (sweep) {
             // onesweep: one launch per pass, no histogram pass, no table scan
             const uint64_t ntiles = (n + kSweepTile - 1) / kSweepTile;
-            CK(grow(c->ticket, sizeof(uint32_t) * 4));
-            if (c->lb_cap < ntiles * kRadix) {
-                CK(grow(c->lbstat, sizeof(uint64_t) * ntiles * kRadix));
-                c->lb_cap = c->lbstat.cap / sizeof(uint64_t);
-                HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));  // epoch 0 = never published
-                c->lb_epoch = 0;
-            }
-            if (++c->lb_epoch >= (1u << 24)) {  // the 24-bit epoch wraps: clear once
-                HIPCK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->st));
-                c->lb_epoch = 1;
-            }
-            HIPCK(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->st));
+            CK(lookback_pass(c, ntiles * kRadix));
             if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
             k_onesweep<kSweepThreads, kSweepItems><<<(uint32_t)ntiles, kSweepThreads, 0, c->st>>>(
                 src, dst, n, shift, db, dhist + kLaterDigits * kRadix + (uint64_t)(pass - 1) * kRadix,
@@ -368,13 +378,6 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false
         c->U = 0;
         return II_OK;
     }
-    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kUniqTile - 1) / kUniqTile);
-    const uint64_t chunk = ((n + nch - 1) / nch + kUniqTile - 1) / kUniqTile * kUniqTile;
-    nch = (n + chunk - 1) / chunk;
-    uint64_t* part = P_<uint64_t>(c->partial);
-    k_uniq_reduce<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part);
-    k_scan_partials<<<1, kBlock, 0, c->st>>>(part, (uint32_t)nch, ps + c->V);
-    k_scan_partials<<<1, kBlock, 0, c->st>>>(part + kMaxChunks, (uint32_t)nch, totals + 6);
     uint64_t* ps_k = ps;  // starts / ends by record key
     uint64_t* pe_k = pe;
     if (wid) {
@@ -383,7 +386,12 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false
         ps_k = P_<uint64_t>(c->pstart_w);
         pe_k = P_<uint64_t>(c->pstop_w);
     }
-    k_uniq_apply<<<(uint32_t)nch, kBlock, 0, c->st>>>(r, n, chunk, part, uniq, Pp, ps_k, pe_k);
+    // one pass with decoupled look-back (k_uniq_sweep): U -> post_start[V], posting bytes -> totals[6]
+    const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
+    CK(lookback_pass(c, 2 * ntiles));
+    k_uniq_sweep<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(r, n, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
+                                                         P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
+                                                         P_<unsigned long long>(c->counters) + C_OVERFLOW);
     k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     if (wid)
         k_wid_post<<<grid_for(c->V), kBlock, 0, c->st>>>(P_<uint32_t>(c->widl), (uint32_t)c->V, ps_k, pe_k, ps, pe);
@@ -575,7 +583,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
                                                            P_<uint32_t>(c->chunk_files));
         k_long_totals<<<1, 64, 0, c->st>>>(counters);
         HIPCK(hipEventRecord(c->ev_res[1], c->st));
-        CK(run_reduce(c, OpU32{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
+        CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
         uint64_t cnt[C_LONGMAX + 1];

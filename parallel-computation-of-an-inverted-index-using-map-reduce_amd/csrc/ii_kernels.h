@@ -12,6 +12,8 @@
 //   K4 final order     qsort by (df desc, word asc), main.c:55-64, 215
 //   K5 k_fmt_*         writer, main.c:227-234 (IDs ascending: main.c:217-226)
 #pragma once
+#include <type_traits>
+
 #include "ii_prims.h"
 
 namespace ii {
@@ -661,10 +663,15 @@ __device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t matc
 }
 
 // Unresolved token of a chunk (K1b -> K1c), one u32: chunk-relative start
-// (16 bits) | chunk-relative token index << 16 (15 bits) | general path << 31.
-// A fast-path miss leaves its key in its record slot.
-constexpr uint32_t kPendSlow = 1u << 31;
+// (16 bits) | chunk-relative token index << 16.  A chunk's list holds its
+// fast-path misses (the key left in the record slot) from the front of its
+// region and its general-path tokens from the back; pend_cnt[c] = the two
+// counts (low / high 16 bits).  The region is the chunk's record range, and
+// there are at most as many pending tokens as tokens.
 static_assert(kChunk <= 65536 && kChunkCap <= 32768, "pending-token fields");
+__device__ __forceinline__ uint64_t pend_limit(const uint64_t* chunk_off, uint64_t cap, uint64_t cbase, uint64_t c) {
+    return cap ? cbase + cap : chunk_off[c + 1];  // dense: chunk_off is the exclusive scan of the counts
+}
 
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram.
@@ -689,8 +696,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
     const uint32_t rot = chunk_rot(c);
     const uint64_t lt = lanemask_lt();
-    uint32_t out = 0;    // records emitted so far (wave-uniform)
-    uint32_t npend = 0;  // tokens left to K1c (wave-uniform)
+    uint32_t out = 0;               // records emitted so far (wave-uniform)
+    uint32_t npf = 0, nps = 0;      // tokens left to K1c: fast-path misses, general-path tokens
+    const uint64_t pend_end = pend_limit(chunk_off, cap, cbase, c);
     if (l < 32) W.hist[l] = 0;
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
@@ -731,7 +739,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
         }
         wave_sync();
         const uint32_t pbase = (uint32_t)(lo - chunk_lo);
-        // 3. keys + cooperative hot-bucket probes, one token per lane
+        // 3. keys + cooperative hot-bucket probes, one token per lane (issuing
+        //    the next batch's probes before resolving this one measured slower:
+        //    13.4 -> 14.6 ms at 10 GB, the extra registers cost a wave per SIMD)
         for (uint32_t b0 = 0; b0 < ntok; b0 += 64) {
             const uint32_t q = b0 + l;
             const bool valid = q < ntok;
@@ -739,7 +749,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             TokKey tk{0ull, 0u, 0u};
             const bool fast = valid && round_fast_key(W.text, W.mask, p, tk);
             const uint32_t home = hot_slot(tk.key, tab.seed);
-            if (!(kAblate & 4) && fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS; same-letter lanes serialize in the LDS unit, not in VALU
+            if (!(kAblate & 4) && fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS: same-letter lanes serialize in the LDS unit, not in VALU
             uint32_t slot = kSlotNone;
             if (kAblate & 1) {
                 if (fast) slot = home;
@@ -758,19 +768,22 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             } else if (fast) {
                 rec[ri] = tk.key;
             }
-            const bool pending = valid && !resolved;
-            const uint64_t pm = __ballot(pending);
-            if (pending)
-                pend[cbase + npend + (uint32_t)__popcll(pm & lt)] =
-                    (pbase + p) | ((out + q) << 16) | (fast ? 0u : kPendSlow);
-            npend += (uint32_t)__popcll(pm);
+            // pending: fast-path misses from the front of the chunk's list, general-path tokens
+            // from its back, so that K1c runs each kind without divergence
+            const bool pf = fast && !resolved, ps = valid && !fast;
+            const uint64_t mf = __ballot(pf), ms = __ballot(ps);
+            const uint32_t e = (pbase + p) | ((out + q) << 16);
+            if (pf) pend[cbase + npf + (uint32_t)__popcll(mf & lt)] = e;
+            if (ps) pend[pend_end - 1 - (nps + (uint32_t)__popcll(ms & lt))] = e;
+            npf += (uint32_t)__popcll(mf);
+            nps += (uint32_t)__popcll(ms);
         }
         out += ntok;
     }
     wave_sync();
     if (l < 26) chunk_hist[c * 26 + l] = W.hist[l];
     if (l == 0) {
-        pend_cnt[c] = npend;
+        pend_cnt[c] = npf | (nps << 16);
         if (cap) chunk_off[c] = out;  // fixed-capacity layout: the chunk's token count
     }
 }
@@ -793,8 +806,8 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
     __shared__ uint32_t s_hist[kWG][32];
     const uint64_t c = wave_chunk();
     if (c >= nch) return;
-    const uint32_t n = pend_cnt[c];
-    if (n == 0) return;
+    const uint32_t pc = pend_cnt[c];
+    if (pc == 0) return;
     const int l = lane_id();
     uint32_t* hist = s_hist[c - (uint64_t)blockIdx.x * kWG];
     if (l < 32) hist[l] = 0;
@@ -803,47 +816,55 @@ __global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restric
     const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
     const bool fsame = f_lo == f_hi;
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
+    const uint64_t pend_end = pend_limit(chunk_off, cap, cbase, c);
     const uint32_t rot = chunk_rot(c);
     const uint64_t lt = lanemask_lt();
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + l;
-        bool is_long = false;
-        uint64_t pos = 0, slot = 0;
-        if (i < n) {
-            const uint32_t e = pend[cbase + i];
-            pos = chunk_lo + (e & 0xFFFFu);
-            const uint64_t r = rec_slot(cbase, cap, rot, (e >> 16) & 0x7FFFu);
-            uint64_t key;
-            uint32_t nlet = 0;
-            if (e & kPendSlow) {
-                const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
-                atomicAdd(&hist[k.first], 1u);
-                key = k.key;
-                nlet = k.nlet;
-            } else {
-                key = rec[r];
+    // kSlow: general-path tokens (key from the text); else fast-path misses (key in the record slot)
+    auto resolve = [&](auto slow_tag, uint32_t n) {
+        constexpr bool kSlow = decltype(slow_tag)::value;
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + l;
+            bool is_long = false;
+            uint64_t pos = 0, slot = 0;
+            if (i < n) {
+                const uint32_t e = kSlow ? pend[pend_end - 1 - i] : pend[cbase + i];
+                pos = chunk_lo + (e & 0xFFFFu);
+                const uint64_t r = rec_slot(cbase, cap, rot, e >> 16);
+                uint64_t key;
+                if (kSlow) {
+                    const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0,
+                                                 tab.seed, 0);
+                    atomicAdd(&hist[k.first], 1u);
+                    key = k.key;
+                    is_long = k.nlet > 12;
+                } else {
+                    key = rec[r];
+                }
+                slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
+                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
+                rec[r] = (slot << 32) | f;
             }
-            slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-            const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
-            rec[r] = (slot << 32) | f;
-            is_long = nlet > 12;
-        }
-        // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
-        const uint64_t lm = __ballot(is_long);
-        if (lm) {
-            const uint32_t shard = (uint32_t)(c & (kLongShards - 1));
-            const int leader = __builtin_ctzll(lm);
-            unsigned long long base = 0;
-            if (l == leader)
-                base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard], (unsigned long long)__popcll(lm));
-            base = (unsigned long long)__shfl((long long)base, leader, 64);
-            if (is_long) {
-                const uint64_t g = base + (uint64_t)__popcll(lm & lt);
-                if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
-                else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+            if (!kSlow) continue;
+            // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
+            const uint64_t lm = __ballot(is_long);
+            if (lm) {
+                const uint32_t shard = (uint32_t)(c & (kLongShards - 1));
+                const int leader = __builtin_ctzll(lm);
+                unsigned long long base = 0;
+                if (l == leader)
+                    base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard],
+                                     (unsigned long long)__popcll(lm));
+                base = (unsigned long long)__shfl((long long)base, leader, 64);
+                if (is_long) {
+                    const uint64_t g = base + (uint64_t)__popcll(lm & lt);
+                    if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
+                    else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+                }
             }
         }
-    }
+    };
+    resolve(std::false_type{}, pc & 0xFFFFu);
+    resolve(std::true_type{}, pc >> 16);
     wave_sync();
     if (l < 26 && hist[l]) chunk_hist[c * 26 + l] += hist[l];
 }
@@ -1382,87 +1403,136 @@ __device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
     return (x & 0xFFFFull) + ((x >> 16) & 0xFFFFull) + ((x >> 32) & 0xFFFFull) + (x >> 48);
 }
 
-// part[b] = distinct pairs of workgroup b's range, part[kMaxChunks + b] = their posting bytes
-__global__ __launch_bounds__(kBlock) void k_uniq_reduce(const uint64_t* __restrict__ rec, uint64_t n, uint64_t chunk,
-                                                        uint64_t* __restrict__ part) {
-    __shared__ uint64_t lds[2][kWaves];
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    uint64_t ac = 0, ab = 0;
-    constexpr int kAhead = 4;  // tiles in flight per iteration (a read-only pass)
-    for (uint64_t base = lo; base < hi; base += kAhead * kUniqTile) {
-        UniqTile u[kAhead];
+// K3 in one pass (decoupled look-back, as k_onesweep): a workgroup takes a
+// tile of kUniqSub sub-tiles (kUniqTile records each) from a ticket, scans
+// them, publishes the tile's distinct
+// pairs and posting bytes (two 8-byte granules: epoch << 40 | flag | value),
+// walks back over the earlier tiles' granules for its starting pair index
+// and byte offset, and writes uniq / P / post_start / post_end.  The records
+// are read once instead of twice.  The last tile also writes the totals:
+// *U_out = distinct pairs, *B_out = posting bytes.
+constexpr int kUniqSub = 4;  // 1, 2, 8 sub-tiles: 5.65, 3.51, 4.83 ms against 2.94 at 10 GB (ticket rate, occupancy)
+constexpr int kUniqSweepTile = kUniqSub * kUniqTile;  // 4096 records
+__global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
+                                                       uint64_t* __restrict__ uniq, uint64_t* __restrict__ P,
+                                                       uint64_t* __restrict__ post_start, uint64_t* __restrict__ post_end,
+                                                       uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
+                                                       uint64_t epoch, uint64_t* __restrict__ U_out,
+                                                       uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err) {
+    __shared__ uint64_t s_rec[kUniqSweepTile + 1];  // [0]: the record before the tile; the tile from [1]
+    __shared__ uint64_t lds[2 * kWaves];
+    __shared__ uint64_t s_ex[kUniqSub][2][kBlock];  // per sub-tile and thread: exclusive pair / byte offsets (16-bit fields)
+    __shared__ uint64_t s_tot[kUniqSub][2];         // per sub-tile: pair / byte totals (16-bit fields)
+    __shared__ uint64_t s_base[2];
+    __shared__ uint32_t s_tile;
+    const int t = threadIdx.x;
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
+    const uint64_t lo = tile * kUniqSweepTile, hi = lo + kUniqSweepTile < n ? lo + kUniqSweepTile : n;
+    // the tile (and the record before it) staged in LDS: scanned, then written after the look-back
+    {
+        uint64_t v[kUniqSweepTile / kBlock];
 #pragma unroll
-        for (int a = 0; a < kAhead; a++) uniq_load(rec, base + (uint64_t)a * kUniqTile, hi, u[a]);
-#pragma unroll
-        for (int a = 0; a < kAhead; a++) {
-            uint64_t pv[kUniqItems], c, b;
-            uniq_eval(u[a], base + (uint64_t)a * kUniqTile, hi, pv, c, b);
-            ac += field16_sum(c);
-            ab += field16_sum(b);
+        for (int j = 0; j < kUniqSweepTile / kBlock; j++) {
+            const uint64_t i = lo + (uint64_t)j * kBlock + t;
+            v[j] = i < hi ? rec[i] : ~0ull;
         }
-    }
-    ac = wave_sum(ac);
-    ab = wave_sum(ab);
-    if (lane_id() == 0) {
-        lds[0][wave_id()] = ac;
-        lds[1][wave_id()] = ab;
+#pragma unroll
+        for (int j = 0; j < kUniqSweepTile / kBlock; j++) s_rec[1 + j * kBlock + t] = v[j];
+        if (t == 0) s_rec[0] = lo > 0 ? rec[lo - 1] : ~0ull;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t tc = 0, tb = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; w++) {
-            tc += lds[0][w];
-            tb += lds[1][w];
-        }
-        part[blockIdx.x] = tc;
-        part[kMaxChunks + blockIdx.x] = tb;
-    }
-}
-
-// Records are keyed by wid or lexid; uniq pairs keep the key, post_start[key]
-// = the word's first pair, post_end[key] = one past its last (the last word's
-// end is set by k_post_last; wid-keyed starts/ends go to lexids in k_wid_post).
-__global__ __launch_bounds__(kBlock) void k_uniq_apply(const uint64_t* __restrict__ rec, uint64_t n, uint64_t chunk,
-                                                       const uint64_t* __restrict__ part, uint64_t* __restrict__ uniq,
-                                                       uint64_t* __restrict__ P, uint64_t* __restrict__ post_start,
-                                                       uint64_t* __restrict__ post_end) {
-    __shared__ uint64_t lds[2 * kWaves];
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    uint64_t run_c = part[blockIdx.x], run_b = part[kMaxChunks + blockIdx.x];
-    UniqTile nx;  // the next tile's records load while this one is scanned and written
-    if (lo < hi) uniq_load(rec, lo, hi, nx);
-    for (uint64_t base = lo; base < hi; base += kUniqTile) {
-        uint64_t r[kUniqItems], pv[kUniqItems], c, b, ec, eb, tc, tb;
-        const UniqTile cur = nx;
-#pragma unroll
-        for (int q = 0; q < kUniqItems; q++) r[q] = cur.r[q];
-        uniq_eval(cur, base, hi, pv, c, b);
-        if (base + kUniqTile < hi) uniq_load(rec, base + kUniqTile, hi, nx);
-        // 16-bit fields: no carries (a field sums at most kBlock pairs of <= 11 bytes)
-        block_excl_scan2(c, b, ec, eb, tc, tb, lds);
-        uint64_t rc = run_c, rb = run_b;
+    // item (k, q) of this thread: tile index k * kUniqTile + q * kBlock + t (coalesced)
+    auto item = [&](int k, int q, uint64_t& r, uint64_t& pv) {
+        const uint32_t x = (uint32_t)(k * kUniqTile + q * kBlock + t);
+        r = s_rec[1 + x];
+        pv = s_rec[x];
+    };
+    uint64_t C = 0, B = 0;
+#pragma unroll 1
+    for (int k = 0; k < kUniqSub; k++) {
+        uint64_t c = 0, b = 0;
 #pragma unroll
         for (int q = 0; q < kUniqItems; q++) {
-            if ((c >> (16 * q)) & 1ull) {
-                const uint64_t u = rc + ((ec >> (16 * q)) & 0xFFFFull);
-                const uint32_t key = (uint32_t)(r[q] >> 32);
-                uniq[u] = r[q];
-                const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
-                const bool wstart = i == 0 || key != (uint32_t)(pv[q] >> 32);
+            uint64_t r, pv;
+            item(k, q, r, pv);
+            const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
+            if (i < hi && (i == 0 || r != pv)) {
+                c |= 1ull << (16 * q);
+                b += (uint64_t)(id_digits((r & 0xFFFFFFFFull) + 1) + 1) << (16 * q);
+            }
+        }
+        // 16-bit fields: no carries (a field sums at most kBlock pairs of <= 11 bytes)
+        uint64_t ec, eb, tc, tb;
+        block_excl_scan2(c, b, ec, eb, tc, tb, lds);
+        s_ex[k][0][t] = ec | (c & 0x0001000100010001ull) << 15;  // the item's own flag rides in bit 15 of its field
+        s_ex[k][1][t] = eb;
+        if (t == 0) {
+            s_tot[k][0] = tc;
+            s_tot[k][1] = tb;
+        }
+        C += field16_sum(tc);
+        B += field16_sum(tb);
+    }
+    // look-back: thread 0 walks the pair counts, thread 1 the byte counts
+    if (t < 2) {
+        const uint64_t v0 = t == 0 ? C : B;
+        uint64_t* mine = status + 2 * tile + t;
+        const uint64_t ep = epoch << 40;
+        uint64_t excl = 0;
+        __hip_atomic_store(mine, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint64_t p = tile; p-- > 0;) {
+            const uint64_t* e = status + 2 * p + t;
+            uint64_t v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {  // tile p's workgroup is running it
+                if (spin == (1u << 24)) {
+                    atomicOr(err, kLbTimeout);
+                    v = ep | kLbFlagP;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            excl += v & kLbValMask;
+            if (v & kLbFlagP) break;
+        }
+        if (tile != 0)
+            __hip_atomic_store(mine, ep | kLbFlagP | (excl + v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_base[t] = excl;
+        if (tile == ntiles - 1) {
+            if (t == 0) *U_out = excl + v0;
+            else *B_out = excl + v0;
+        }
+    }
+    __syncthreads();
+    uint64_t rc = s_base[0], rb = s_base[1];
+#pragma unroll 1
+    for (int k = 0; k < kUniqSub; k++) {
+        const uint64_t ec = s_ex[k][0][t], eb = s_ex[k][1][t], tc = s_tot[k][0], tb = s_tot[k][1];
+#pragma unroll
+        for (int q = 0; q < kUniqItems; q++) {
+            const uint64_t f = (ec >> (16 * q)) & 0xFFFFull;
+            if (f & 0x8000ull) {
+                uint64_t r, pv;
+                item(k, q, r, pv);
+                const uint64_t uu = rc + (f & 0x7FFFull);
+                const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
+                uniq[uu] = r;
+                const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
+                const bool wstart = i == 0 || key != pkey;
                 // P is read at word starts (k_fmt_words, OpLineOff) and at the
                 // first posting of every 64 (k_fmt_posts) only
-                if (wstart || (u & 63u) == 0) P[u] = rb + ((eb >> (16 * q)) & 0xFFFFull);
+                if (wstart || (uu & 63u) == 0) P[uu] = rb + ((eb >> (16 * q)) & 0xFFFFull);
                 if (wstart) {
-                    post_start[key] = u;
-                    if (i > 0) post_end[(uint32_t)(pv[q] >> 32)] = u;
+                    post_start[key] = uu;
+                    if (i > 0) post_end[pkey] = uu;
                 }
             }
             rc += (tc >> (16 * q)) & 0xFFFFull;
             rb += (tb >> (16 * q)) & 0xFFFFull;
         }
-        run_c = rc;
-        run_b = rb;
     }
 }
 

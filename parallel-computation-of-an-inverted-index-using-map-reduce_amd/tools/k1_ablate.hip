@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < p.nfiles; i++) ids[i] = i;
     CK(hipMalloc(&fstart, 8 * p.nfiles)); CK(hipMemcpy(fstart, off.data(), 8 * p.nfiles, hipMemcpyHostToDevice));
     CK(hipMalloc(&fid, 4 * p.nfiles)); CK(hipMemcpy(fid, ids.data(), 4 * p.nfiles, hipMemcpyHostToDevice));
-    CK(hipMalloc(&chunk, 8 * nch)); CK(hipMalloc(&chist, 4 * 26 * nch)); CK(hipMalloc(&counters, 8 * C_NUM));
+    CK(hipMalloc(&chunk, 8 * (nch + 1))); CK(hipMalloc(&chist, 4 * 26 * nch)); CK(hipMalloc(&counters, 8 * C_NUM));
     CK(hipMalloc(&keys, 8 * nslots)); CK(hipMalloc(&rep, 8 * nslots)); CK(hipMalloc(&longs, sizeof(LongTok) * lcap));
     // count pass -> offsets (host scan)
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
@@ -99,11 +99,12 @@ int main(int argc, char** argv) {
     k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms_count; CK(hipEventElapsedTime(&ms_count, a, b));
-    std::vector<uint64_t> cnt(nch);
+    std::vector<uint64_t> cnt(nch + 1);
     CK(hipMemcpy(cnt.data(), chunk, 8 * nch, hipMemcpyDeviceToHost));
     uint64_t T = 0;
-    for (auto& c : cnt) { uint64_t x = c; c = T; T += x; }
-    CK(hipMemcpy(chunk, cnt.data(), 8 * nch, hipMemcpyHostToDevice));
+    for (uint64_t c = 0; c < nch; c++) { uint64_t x = cnt[c]; cnt[c] = T; T += x; }
+    cnt[nch] = T;  // chunk_off[c + 1] bounds chunk c's pending list (dense layout)
+    CK(hipMemcpy(chunk, cnt.data(), 8 * (nch + 1), hipMemcpyHostToDevice));
     CK(hipMalloc(&rec, 8 * T));
     uint32_t *pend, *pcnt;
     CK(hipMalloc(&pend, 4 * T)); CK(hipMalloc(&pcnt, 4 * nch));
