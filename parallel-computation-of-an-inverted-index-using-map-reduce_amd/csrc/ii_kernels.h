@@ -573,11 +573,27 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x) {
     return (r & 0x3FFu) | ((r >> 6) & 0xFFC00u);                // b0@15 b1@10 b2@5 b3@0
 }
 
-// Register key path of the cleaning loop (main.c:105-111) for the common
-// token: its letters form one run from its first byte, at most 12 of them,
-// ended by whitespace / NUL (trailing punctuation allowed).  The masks come
-// from the round's window masks, the letters are 12 bytes read from LDS.
-// Returns false for every other token (general path).
+// Byte g (0..15) of the 16-byte value x[0..3] removed: the bytes above it
+// move down one place.
+__device__ __forceinline__ void drop_byte(uint32_t (&x)[4], uint32_t g) {
+    const uint32_t s[4] = {__builtin_amdgcn_alignbyte(x[1], x[0], 1), __builtin_amdgcn_alignbyte(x[2], x[1], 1),
+                           __builtin_amdgcn_alignbyte(x[3], x[2], 1), x[3] >> 8};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int kb = (int)g - 4 * i;  // bytes of dword i that stay
+        const uint32_t m = kb >= 4 ? 0xFFFFFFFFu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1u;
+        x[i] = (x[i] & m) | (s[i] & ~m);
+    }
+}
+
+// Register key path of the cleaning loop (main.c:105-111): the token ends
+// (whitespace / NUL) within reach of the round's masks and keeps 1..12
+// letters; letters in one run from its first byte (plain or capitalised
+// words, trailing punctuation), or — within its first 16 bytes — with up to
+// three other bytes among them (a leading bracket, an apostrophe, a 2-byte
+// UTF-8 letter: main.c:105-111 drops them), which are removed from the 16
+// bytes read from LDS before the 5-bit packing.  Returns false for every
+// other token (general path, K1c).
 __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint32_t* s_mask, uint32_t p, TokKey& k) {
     const uint32_t w0 = p >> 4, sh = p & 15u;
     const uint32_t m0 = s_mask[w0], m1 = s_mask[w0 + 1];
@@ -587,17 +603,26 @@ __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint
     const uint32_t e = __builtin_ctz(term);
     const uint32_t lm = let & ((1u << e) - 1u);
     const uint32_t n = __popc(lm);
-    if (n == 0 || n > 12 || lm != (1u << n) - 1u) return false;
+    if (n == 0 || n > 12) return false;
     const uint32_t a = 16u + p, al = a & 3u;
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_text) + (a >> 2);
-    const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2], d3 = s32[3];
-    const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, al);
-    const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, al);
-    const uint32_t x2 = __builtin_amdgcn_alignbyte(d3, d2, al);
-    const uint64_t key = ((uint64_t)pack4(x0) << 44) | ((uint64_t)pack4(x1) << 24) | ((uint64_t)pack4(x2) << 4);
+    const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2], d3 = s32[3], d4 = s32[4];
+    uint32_t x[4] = {__builtin_amdgcn_alignbyte(d1, d0, al), __builtin_amdgcn_alignbyte(d2, d1, al),
+                     __builtin_amdgcn_alignbyte(d3, d2, al), __builtin_amdgcn_alignbyte(d4, d3, al)};
+    if (lm != (1u << n) - 1u) {  // other bytes before or among the letters
+        if (e > 16) return false;
+        uint32_t gaps = ~lm & ((2u << (31 - __builtin_clz(lm))) - 1u);  // below the last letter
+        if (__popc(gaps) > 3) return false;
+        while (gaps) {  // from the highest down: the lower positions stay put
+            const uint32_t g = 31 - __builtin_clz(gaps);
+            drop_byte(x, g);
+            gaps &= ~(1u << g);
+        }
+    }
+    const uint64_t key = ((uint64_t)pack4(x[0]) << 44) | ((uint64_t)pack4(x[1]) << 24) | ((uint64_t)pack4(x[2]) << 4);
     k.key = key & (~0ull << (64 - 5 * n));
     k.nlet = n;
-    k.first = (x0 & 31u) - 1u;
+    k.first = (x[0] & 31u) - 1u;
     return true;
 }
 
