@@ -626,49 +626,13 @@ __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint
     return true;
 }
 
-// Cooperative probe of the hot table: 32 tokens per load round, 2 rounds; a
-// lane pair loads the two 16-B slot pairs that begin the key's probe order in
-// its 8-slot bucket (home's pair and the next one), so one load instruction
-// touches one 64-B bucket per lane pair instead of four lines per lane.  A
-// frequent word sits at or next to its home slot (it was inserted while its
-// bucket was still empty), so the short window decides almost every token;
-// the rest go to K1c.  known = the slots seen.
-struct ProbeParts {
-    ulonglong2 q[2];
-};
-__device__ __forceinline__ void probe_issue(const Table& t, uint32_t home, ProbeParts& pp) {
-    const int l = lane_id();
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const uint32_t h = (uint32_t)__shfl((int)home, 32 * r + (l >> 1), 64);
-        const uint32_t pair = (((h & (kBucket - 1)) >> 1) + (l & 1)) & 3u;
-        pp.q[r] = *reinterpret_cast<const ulonglong2*>(t.keys + (h & ~(uint32_t)(kBucket - 1)) + 2u * pair);
-    }
-}
-__device__ __forceinline__ void probe_finish(uint64_t key, uint32_t home, const ProbeParts& pp, uint32_t& match,
-                                             uint32_t& full, uint32_t& known) {
-    const int l = lane_id();
-    const uint32_t p0 = (home & (kBucket - 1)) >> 1, p1 = (p0 + 1) & 3u;
-    match = full = 0;
-    known = (3u << (2 * p0)) | (3u << (2 * p1));
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const int src = 32 * r + (l >> 1);
-        const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), src, 64) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)key, src, 64);
-        const uint64_t m0 = __ballot(pp.q[r].x == k), m1 = __ballot(pp.q[r].y == k);
-        const uint64_t f0 = __ballot(pp.q[r].x != 0ull), f1 = __ballot(pp.q[r].y != 0ull);
-        if ((l >> 5) == r) {
-            const int b = 2 * (l & 31);
-            const uint32_t a0 = (uint32_t)(m0 >> b) & 3u, a1 = (uint32_t)(m1 >> b) & 3u;
-            const uint32_t c0 = (uint32_t)(f0 >> b) & 3u, c1 = (uint32_t)(f1 >> b) & 3u;
-            match = ((a0 & 1u) << (2 * p0)) | ((a1 & 1u) << (2 * p0 + 1)) | ((a0 >> 1) << (2 * p1)) |
-                    ((a1 >> 1) << (2 * p1 + 1));
-            full = ((c0 & 1u) << (2 * p0)) | ((c1 & 1u) << (2 * p0 + 1)) | ((c0 >> 1) << (2 * p1)) |
-                   ((c1 >> 1) << (2 * p1 + 1));
-        }
-    }
-}
+// Hot-table probe of K1b: a lane loads the two 16-B slot pairs that begin
+// its key's probe order in the 8-slot bucket (home's pair and the next, one
+// 64-B line).  A frequent word sits at or next to its home slot (it was
+// inserted while its bucket was still empty), so the short window decides
+// almost every token; the rest go to K1c.  (Two lanes sharing one token's
+// loads, so that an instruction touches half as many lines, measured 0.35 ms
+// slower at 10 GB: the shuffles that route keys and results cost more VALU.)
 __device__ __forceinline__ uint32_t rotr8(uint32_t x, uint32_t s) { return ((x >> s) | (x << (8 - s))) & 0xFFu; }
 // Lookup from a partly seen bucket: a match is the slot; otherwise the first
 // empty slot inside the seen prefix of the probe order is claimed
@@ -779,11 +743,16 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             if (kAblate & 1) {
                 if (fast) slot = home;
             } else {
-                ProbeParts pp;
-                probe_issue(tab, home, pp);  // all lanes: a lane without a key probes key 0's bucket, harmlessly
-                uint32_t match, full, known;
-                probe_finish(tk.key, home, pp, match, full, known);
-                if (fast) slot = bucket_resolve(tab, match, full, known, tk.key, home, lo + p);
+                // the two 16-B slot pairs that begin the key's probe order in its 8-slot bucket (home's
+                // pair and the next; one 64-B line); a lane without a key probes key 0's bucket, harmlessly
+                const uint32_t h7 = home & (kBucket - 1), bbase = home - h7, p0 = h7 >> 1, p1 = (p0 + 1) & 3u;
+                const ulonglong2 qa = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + 2 * p0);
+                const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + 2 * p1);
+                const uint32_t match = ((uint32_t)(qa.x == tk.key) << (2 * p0)) | ((uint32_t)(qa.y == tk.key) << (2 * p0 + 1)) |
+                                       ((uint32_t)(qb.x == tk.key) << (2 * p1)) | ((uint32_t)(qb.y == tk.key) << (2 * p1 + 1));
+                const uint32_t full = ((uint32_t)(qa.x != 0ull) << (2 * p0)) | ((uint32_t)(qa.y != 0ull) << (2 * p0 + 1)) |
+                                      ((uint32_t)(qb.x != 0ull) << (2 * p1)) | ((uint32_t)(qb.y != 0ull) << (2 * p1 + 1));
+                if (fast) slot = bucket_resolve(tab, match, full, (3u << (2 * p0)) | (3u << (2 * p1)), tk.key, home, lo + p);
             }
             const bool resolved = fast && slot != kSlotNone;
             const uint64_t ri = rec_slot(cbase, cap, rot, out + q);

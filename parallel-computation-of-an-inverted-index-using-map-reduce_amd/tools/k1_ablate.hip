@@ -110,7 +110,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&pend, 4 * T)); CK(hipMalloc(&pcnt, 4 * nch));
     Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters};
 #define RUN(A) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt); \
-    printf("emit ablate %2d: %.3f ms  resolve %.3f ms\n", A, e_, g_res); } while (0)
+    unsigned long long np_ = 0; std::vector<uint32_t> pc_(nch); CK(hipMemcpy(pc_.data(), pcnt, 4 * nch, hipMemcpyDeviceToHost)); \
+    for (auto x : pc_) np_ += (x & 0xFFFFu) + (x >> 16); \
+    printf("emit ablate %2d: %.3f ms  resolve %.3f ms  pending %llu\n", A, e_, g_res, np_); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(0); RUN(1); RUN(4); RUN(5);
     printf("count (best of 5): %.3f ms\n", best_of([&] { k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
