@@ -73,10 +73,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 //              whose hot bucket was already full.
 // A word lives in exactly one place: a probe scans the same bucket (then the
 // same big-table run) in the same order and slots only go empty -> full.
-#ifndef II_HOT_LOG2
-#define II_HOT_LOG2 20  // 2^20: K1c 5.1 -> 3.4 ms at 10 GB vs 2^19 (fewer words overflow to the big table)
-#endif
-constexpr int kHotLog2 = II_HOT_LOG2;  // hot level: 2^20 slots (8 MB of keys) in 8-slot buckets
+constexpr int kHotLog2 = 20;  // hot level: 2^20 slots (8 MB of keys) in 8-slot buckets (vs 2^19: K1c 5.1 -> 3.4 ms
+                              // at 10 GB, fewer words overflow to the big table)
 constexpr uint64_t kHotSlots = 1ull << kHotLog2;
 constexpr int kBucket = 8;
 
@@ -553,9 +551,15 @@ struct RoundRegs {
 };
 __device__ __forceinline__ void fetch_round(RoundRegs& r, const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t lo) {
     const int l = lane_id();
+    r.h = make_uint4(0, 0, 0, 0);
+    if (lo >= 16 && lo + kRoundStaged <= nbytes) {  // (wave-uniform) every piece lies inside the text: plain loads
+#pragma unroll
+        for (int j = 0; j < kWin; j++) r.v[j] = *reinterpret_cast<const uint4*>(text + lo + 16 * (64 * j + l));
+        if (l <= kHaloPieces) r.h = *reinterpret_cast<const uint4*>(text + lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1));
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < kWin; j++) r.v[j] = load16(text, nbytes, (int64_t)lo + 16 * (64 * j + l));
-    r.h = make_uint4(0, 0, 0, 0);
     if (l <= kHaloPieces) r.h = load16(text, nbytes, (int64_t)lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1));
 }
 __device__ __forceinline__ void store_round(uint8_t* s_text, const RoundRegs& r) {
@@ -1237,8 +1241,9 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
     uint64_t o = lo;  // next output position
-    // (prefetching the next tile, deferring the stores by one tile, and
-    // test-before-set in the bitmap all measured no faster)
+    // (prefetching the next tile — 4.52 -> 4.88 ms at 10 GB —, deferring the
+    // stores by one tile, and test-before-set in the bitmap all measured no
+    // faster)
     for (uint64_t tb = lo; tb < hi; tb += kCTile) {
         uint64_t raw[kS0Items];
 #pragma unroll
@@ -1470,34 +1475,53 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
         C += field16_sum(tc);
         B += field16_sum(tb);
     }
-    // look-back: thread 0 walks the pair counts, thread 1 the byte counts
-    if (t < 2) {
-        const uint64_t v0 = t == 0 ? C : B;
-        uint64_t* mine = status + 2 * tile + t;
+    // look-back, wave 0: lanes 0..31 walk the pair counts, lanes 32..63 the
+    // byte counts, each half loading the granules of 32 earlier tiles per
+    // round trip (walking one tile per round trip, the walk fell behind the
+    // rate at which tiles start, so every tile walked far)
+    if (t < 64) {
+        const uint32_t f = (uint32_t)t >> 5, j = (uint32_t)t & 31u;  // field, distance - 1 of the tile this lane loads
+        const uint64_t v0 = f == 0 ? C : B;
         const uint64_t ep = epoch << 40;
+        if (j == 0)
+            __hip_atomic_store(status + 2 * tile + f, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | v0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         uint64_t excl = 0;
-        __hip_atomic_store(mine, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint64_t p = tile; p-- > 0;) {
-            const uint64_t* e = status + 2 * p + t;
-            uint64_t v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {  // tile p's workgroup is running it
-                if (spin == (1u << 24)) {
-                    atomicOr(err, kLbTimeout);
-                    v = ep | kLbFlagP;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+        bool done = tile == 0;
+        for (int64_t base = (int64_t)tile - 1; __ballot(!done) != 0; base -= 32) {
+            uint64_t v = ep | kLbFlagP;  // before tile 0: an inclusive prefix of 0
+            const int64_t p = base - (int64_t)j;
+            if (!done && p >= 0) {
+                const uint64_t* e = status + 2 * (uint64_t)p + f;
                 v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {  // tile p's workgroup is running it
+                    if (spin == (1u << 24)) {
+                        atomicOr(err, kLbTimeout);
+                        v = ep | kLbFlagP;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
-            excl += v & kLbValMask;
-            if (v & kLbFlagP) break;
+            // this half's nearest inclusive prefix ends its walk
+            const uint32_t q = (uint32_t)(__ballot((v & kLbFlagP) != 0) >> (32 * f));
+            const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 31u;
+            uint64_t add = (!done && j <= upto) ? (v & kLbValMask) : 0;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) add += (uint64_t)__shfl_xor((long long)add, o, 64);
+            excl += add;
+            done = done || q != 0;
         }
-        if (tile != 0)
-            __hip_atomic_store(mine, ep | kLbFlagP | (excl + v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_base[t] = excl;
-        if (tile == ntiles - 1) {
-            if (t == 0) *U_out = excl + v0;
-            else *B_out = excl + v0;
+        if (j == 0) {
+            if (tile != 0)
+                __hip_atomic_store(status + 2 * tile + f, ep | kLbFlagP | (excl + v0), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_base[f] = excl;
+            if (tile == ntiles - 1) {
+                if (f == 0) *U_out = excl + v0;
+                else *B_out = excl + v0;
+            }
         }
     }
     __syncthreads();
@@ -1616,13 +1640,10 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
 // with every group's loads (pairs, then the fbase gathers) issued before any
 // digits are written: one dependent load chain per group left the pass
 // latency-bound.  A group reads the posting byte offset of its first posting
-// only (P is written at multiples of 64 and at word starts, k_uniq_apply) and
+// only (P is written at multiples of 64 and at word starts, k_uniq_sweep) and
 // places the rest by a wave scan of their byte counts, so the pass reads
 // 8 bytes per posting instead of 16.
-#ifndef II_FMT_ITEMS
-#define II_FMT_ITEMS 4
-#endif
-constexpr int kFmtItems = II_FMT_ITEMS;
+constexpr int kFmtItems = 4;  // groups per wave (2 or 8: slower)
 __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
                                                       const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
                                                       uint8_t* __restrict__ out) {

@@ -164,13 +164,8 @@ constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
 constexpr int kScatterThreads = 512;              // token-sort scatter: tiles of 512 x 16 keys (runs twice as long
 constexpr int kScatterItems = 16;                  // as 256 x 16: 2.22 -> 1.95 ms per pass at 10 GB; 1024 x 16 and
                                                    // 512 x 24 were slower)
-#ifndef II_SWEEP_NT
-#define II_SWEEP_NT 512
-#endif
-#ifndef II_SWEEP_IT
-#define II_SWEEP_IT 16
-#endif
-constexpr int kSweepThreads = II_SWEEP_NT, kSweepItems = II_SWEEP_IT;
+constexpr int kSweepThreads = 512, kSweepItems = 16;  // onesweep tiles of 8192 keys (512 x 8, 256 x 16: slower —
+                                                      // more tiles for every look-back to walk over)
 constexpr int kSweepTile = kSweepThreads * kSweepItems;  // keys per onesweep tile
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
@@ -279,6 +274,9 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
             if (kHasVals) val[k] = nval[k];
         }
         __syncthreads();
+        // ranks inside the wave (one LDS read-modify-write per item; the
+        // leader-atomic form of k_onesweep measured slower here: 2.10 -> 2.17
+        // ms, its extra registers cost the prefetched tile a wave per SIMD)
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const bool valid = wbase + (uint64_t)k * 64 < hi;
@@ -375,10 +373,15 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
 // MI355X_MICROARCH.md "inter-workgroup visibility"):
 //   bits 63..40 epoch of the pass (entries of other passes read as "not
 //   yet"; no clearing between passes), 39..38 flag, 37..0 count.
-// Same tile shape, ranking and store runs as k_radix_scatter.
+// Same tile shape and store runs as k_radix_scatter; the tile is reordered in
+// LDS before the look-back, which only the global stores need.
 constexpr uint64_t kLbFlagA = 1ull << 38, kLbFlagP = 2ull << 38, kLbValMask = (1ull << 38) - 1;
 constexpr unsigned long long kLbTimeout = 8;  // error bit (counters[C_OVERFLOW]) of a look-back that never resolved
-template <int NT, int IT>
+// kLbPer: look-back entries per lane per round trip (tools/sort_bench.hip, one
+// 7-bit pass over 4.8e8 records: 1 -> 5.7 ms, 2 -> 2.07, 3 -> 2.11, 4 -> 2.18,
+// 8 -> 2.50: too few and the walk falls behind, too many and the granule loads
+// themselves cost).
+template <int NT, int IT, int kLbPer = 2>
 __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                  uint64_t n, int shift, int dbits, const uint64_t* __restrict__ dbase,
                                                  uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
@@ -414,7 +417,12 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
         const uint64_t idx = wbase + (uint64_t)k * 64;
         key[k] = idx < n ? kin[idx] : ~0ull;
     }
-    uint32_t rank[IT];
+    // ranks inside the wave: per item, the lanes sharing a digit (ballots on
+    // its bits); the lowest of them adds the group's size to the wave's digit
+    // counter (LDS atomic with return) and the others take the old count from
+    // it — the items' atomics are independent, so they pipeline in the LDS
+    // unit instead of one read-modify-write round trip per item
+    uint32_t info[IT];  // rank inside the item's group | group size << 8 | leader lane << 16
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const bool valid = wbase + (uint64_t)k * 64 < n;
@@ -428,14 +436,20 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
                 m &= bit ? bb : ~bb;
             }
         }
-        uint32_t r = 0;
-        if (valid) {
-            const uint32_t before = s_wcnt[w][d];
-            r = before + __popcll(m & lt);
-            if ((m & lt) == 0) s_wcnt[w][d] = before + __popcll(m);
-        }
-        rank[k] = r;
+        info[k] = valid ? (uint32_t)__popcll(m & lt) | ((uint32_t)__popcll(m) << 8) | ((uint32_t)__builtin_ctzll(m) << 16)
+                        : 0xFFFFFFFFu;
     }
+    uint32_t before[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        before[k] = 0;
+        if ((info[k] & 0xFFu) == 0u)  // group leader (invalid lanes carry 0xFF)
+            before[k] = atomicAdd(&s_wcnt[w][(uint32_t)(key[k] >> shift) & dmask], (info[k] >> 8) & 0xFFu);
+    }
+    uint32_t rank[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+        rank[k] = (uint32_t)__shfl((int)before[k], (int)((info[k] >> 16) & 63u), 64) + (info[k] & 0xFFu);
     __syncthreads();
     uint32_t cw[NW];
     uint32_t tot_d = 0;
@@ -446,55 +460,16 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
             tot_d += cw[ww];
         }
     }
-    // look-back: publish this tile's count at once, then sum the earlier
-    // tiles' counts — four lanes per digit, each loading the entry of a
-    // different earlier tile, so a chain of A entries is walked four tiles per
-    // round trip
+    // publish this tile's digit counts at once (flag A), so that later tiles
+    // can pass over it while it still reorders
     const uint64_t ep = epoch << 40;
     if (digit_thread) {
         s_tot[t] = tot_d;
         __hip_atomic_store(status + tile * kRadix + t, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | tot_d,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    const uint32_t gj = t & 3;  // place of this lane in its quad
-    for (uint32_t gd = t >> 2; gd < ndig; gd += NT / 4) {  // the quad's digit; control flow is quad-uniform
-        uint64_t excl = 0;
-        for (int64_t base = (int64_t)tile - 1; base >= 0; base -= 4) {
-            const int64_t p = base - (int64_t)gj;
-            uint64_t v = kLbFlagP;  // before tile 0: an inclusive prefix of 0
-            if (p >= 0) {
-                const uint64_t* e = status + (uint64_t)p * kRadix + gd;
-                v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // tile p has not published yet (its workgroup is running); a wait of seconds means a
-                // broken hand-off: flag it and let the launch drain rather than spin forever
-                for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {
-                    if (spin == (1u << 24)) {
-                        atomicOr(err, kLbTimeout);
-                        v = ep | kLbFlagP;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            // the nearest inclusive prefix among the quad's four tiles ends the walk
-            const uint32_t q = (uint32_t)(__ballot((v & kLbFlagP) != 0) >> (lane_id() & ~3)) & 0xFu;
-            const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 3u;
-            uint64_t add = gj <= upto ? (v & kLbValMask) : 0;
-            add += (uint64_t)__shfl_xor((long long)add, 1, 64);
-            add += (uint64_t)__shfl_xor((long long)add, 2, 64);
-            excl += add;
-            if (q) break;
-        }
-        if (gj == 0) {
-            if (tile != 0)
-                __hip_atomic_store(status + tile * kRadix + gd, ep | kLbFlagP | (excl + s_tot[gd]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            s_run[gd] = dbase[gd] + excl;
-        }
-    }
-    // digit t: tile start, per-wave offsets (as k_radix_scatter)
+    // digit t: tile start, per-wave offsets (as k_radix_scatter); the tile is
+    // reordered by digit in LDS before the look-back, which it does not need
     const uint64_t inc = wave_incl_scan(tot_d);
     if (w < kDW && l == 63) s_scan[w] = inc;
     __syncthreads();
@@ -520,6 +495,60 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
         if (wbase + (uint64_t)k * 64 < n) {
             const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
             s_keys[s_wcnt[w][d] + rank[k]] = key[k];
+        }
+    }
+    // look-back: sum the earlier tiles' counts of each digit until an
+    // inclusive prefix (flag P).  Four lanes per digit, each loading the
+    // entries of kLbPer different earlier tiles per round trip: a quad passes
+    // over 4 * kLbPer tiles per round trip.  (At one tile per lane the walk
+    // advanced about as fast as new tiles started, so every tile walked far.)
+    const uint32_t gj = t & 3;  // place of this lane in its quad
+    for (uint32_t gd = t >> 2; gd < ndig; gd += NT / 4) {  // the quad's digit; control flow is quad-uniform
+        uint64_t excl = 0;
+        for (int64_t base = (int64_t)tile - 1; base >= 0; base -= 4 * kLbPer) {
+            uint64_t v[kLbPer];
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++) {  // entry of tile base - (4 u + gj): distance 4 u + gj
+                const int64_t p = base - (int64_t)(4 * u + gj);
+                v[u] = p >= 0 ? __hip_atomic_load(status + (uint64_t)p * kRadix + gd, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : ep | kLbFlagP;  // before tile 0: an inclusive prefix of 0
+            }
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++) {
+                // tile p has not published yet (its workgroup is running); a wait of seconds means a
+                // broken hand-off: flag it and let the launch drain rather than spin forever
+                const int64_t p = base - (int64_t)(4 * u + gj);
+                for (uint32_t spin = 0; (v[u] >> 40) != epoch; spin++) {
+                    if (spin == (1u << 24)) {
+                        atomicOr(err, kLbTimeout);
+                        v[u] = ep | kLbFlagP;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    v[u] = __hip_atomic_load(status + (uint64_t)p * kRadix + gd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            // the nearest inclusive prefix among the quad's tiles ends the walk
+            uint32_t q = 0;
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++)
+                q |= ((uint32_t)(__ballot((v[u] & kLbFlagP) != 0) >> (lane_id() & ~3)) & 0xFu) << (4 * u);
+            const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 4u * kLbPer - 1u;
+            uint64_t add = 0;
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++)
+                if (4u * u + gj <= upto) add += v[u] & kLbValMask;
+            add += (uint64_t)__shfl_xor((long long)add, 1, 64);
+            add += (uint64_t)__shfl_xor((long long)add, 2, 64);
+            excl += add;
+            if (q) break;
+        }
+        if (gj == 0) {
+            if (tile != 0)
+                __hip_atomic_store(status + tile * kRadix + gd, ep | kLbFlagP | (excl + s_tot[gd]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_run[gd] = dbase[gd] + excl;
         }
     }
     __syncthreads();
