@@ -1180,14 +1180,18 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // ---------------------------------------------------------------- K2 first pass
 // First pass of the token sort over the records in text order
 // (slot << 32 | file id0), one workgroup per contiguous range, tiles of
-// kSortTile records with the scatter's item mapping:
+// kCTile records with the scatter's item mapping:
 //  * drops repeated (hot word, file) records: a record whose slot is a
 //    hot-table slot and whose file is the tile's epoch file is dropped when
 //    the same slot was already kept in this epoch (LDS bitmap, cleared when
-//    the epoch changes; the epoch is the file id0 of each tile's first
-//    record).  Only exact duplicates go, and which copy survives does not
-//    matter, so K3 still sees every distinct (word, file) pair;
-//  * replaces the slot by the word's lexicographic id (remap);
+//    the epoch changes; the epoch of a tile is the file of the previous
+//    tile's last record — what every thread knows after that tile's barrier,
+//    so a tile costs one barrier, and two when the file changes).  Only exact
+//    duplicates go, and which copy survives does not matter, so K3 still sees
+//    every distinct (word, file) pair;
+//  * replaces the slot by the word's sort key (remap: lexicographic id, or
+//    with kWid the word id — the hot slot itself, remap only for big-table
+//    words);
 //  * writes the kept records, in order, to kout[lo ...) and counts their
 //    pass-0 digit (digit-major table, as k_radix_hist).
 // Workgroup b takes the K1b chunks [b * group, (b + 1) * group): virtual
@@ -1198,9 +1202,11 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // voff[c0], the range pass 0's scatter reads back.
 // The dedup bitmap covers the whole hot level (1 bit per slot in LDS, 128
 // KiB: one 1024-thread workgroup per CU; covering only half of it doubled
-// the sort time).  The kept records' later radix digits are counted here too
-// (dhist, global atomics per workgroup): the onesweep passes that follow need
-// only those global counts, not a per-tile histogram pass.
+// the sort time, and a 64 KiB direct-mapped cache of kept records — two
+// workgroups per CU — kept 0.50 T records instead of 0.34 T: the frequent
+// words' entries were evicted by the rare ones).  The kept records' later
+// radix digits are counted here too (dhist, global atomics per workgroup):
+// the onesweep passes that follow need only those global counts.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
 constexpr int kCBlock = 1024;                   // 16 waves share one 128 KiB dedup bitmap
 constexpr int kS0Items = 8;                     // records per thread per tile
@@ -1222,15 +1228,15 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     __shared__ uint32_t bm[kDedupWords];
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
     __shared__ uint32_t s_later[kLaterDigits][kRadix];
-    __shared__ uint32_t s_wtot[kCWaves];
-    __shared__ uint32_t s_epoch, s_flag;
+    __shared__ uint32_t s_wtot[2][kCWaves];      // per tile parity: one barrier per tile
+    __shared__ uint32_t s_last[2];               // per tile parity: file of the tile's last record
     const int w = wave_id(), l = lane_id();
     const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
     for (int i = threadIdx.x; i < kCWaves * kRadix; i += kCBlock) (&cnt[0][0])[i] = 0;
     for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += kCBlock) (&s_later[0][0])[i] = 0;
+    for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
     for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
-    if (threadIdx.x == 0) s_epoch = 0xFFFFFFFFu;  // the first tile always starts an epoch
     __syncthreads();
     const uint64_t tofs = (uint64_t)w * 64 * kS0Items + l;
     const uint64_t lt = lanemask_lt();
@@ -1241,11 +1247,11 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
     uint64_t o = lo;  // next output position
-    // (prefetching the next tile — 4.52 -> 4.88 ms at 10 GB —, deferring the
-    // stores by one tile, and test-before-set in the bitmap all measured no
-    // faster)
-    for (uint64_t tb = lo; tb < hi; tb += kCTile) {
-        uint64_t raw[kS0Items];
+    // The next tile's records are loaded while this one is written: issued
+    // after this tile's remap gathers have been consumed (vmcnt is in order, so
+    // a prefetch issued before them would make the gathers wait for it).
+    uint64_t nraw[kS0Items];
+    auto load_tile = [&](uint64_t tb) {
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
@@ -1263,19 +1269,22 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                 }
                 src = gbase + ((ri + gadj) & (uint32_t)(kChunkCap - 1));
             }
-            raw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
+            nraw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
         }
-        if (threadIdx.x == 0) {  // thread 0's item 0 is the tile's first record
-            const uint32_t f = (uint32_t)raw[0];
-            s_flag = f != s_epoch;
-            s_epoch = f;
-        }
-        __syncthreads();
-        if (s_flag) {
+    };
+    if (lo < hi) load_tile(lo);
+    // the first tile's epoch: the file of the range's first record (every lane loads it)
+    uint32_t epoch = lo < hi ? (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo] : 0u;
+    uint32_t par = 0;
+    for (uint64_t tb = lo; tb < hi; tb += kCTile, par ^= 1u) {
+        uint64_t raw[kS0Items];
+#pragma unroll
+        for (int k = 0; k < kS0Items; k++) raw[k] = nraw[k];
+        if (tb != lo && s_last[par ^ 1u] != epoch) {  // (workgroup-uniform) a new file: clear the bitmap
+            epoch = s_last[par ^ 1u];
             for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
             __syncthreads();
         }
-        const uint32_t epoch = s_epoch;
         uint32_t keep = 0, wcount = 0;
         uint32_t pos[kS0Items];
 #pragma unroll
@@ -1291,7 +1300,6 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             wcount += (uint32_t)__popcll(b);
             keep |= (uint32_t)ok << k;
         }
-        // the remap gathers of the kept records are in flight across the barrier
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)  // slot -> sort key, in place
             if ((keep >> k) & 1u) {
@@ -1300,15 +1308,21 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                 const uint32_t key = (kWid && slot < kHotSlots) ? slot : remap[slot];
                 raw[k] = ((uint64_t)key << 32) | (raw[k] & 0xFFFFFFFFull);
             }
-        if (l == 0) s_wtot[w] = wcount;
-        __syncthreads();
+        if (l == 0) s_wtot[par][w] = wcount;
+        // the tile's last record (thread kCBlock - 1, item kS0Items - 1; or the range's last)
+        const uint64_t last = tb + kCTile < hi ? tb + kCTile - 1 : hi - 1;
+#pragma unroll
+        for (int k = 0; k < kS0Items; k++)
+            if (tb + tofs + (uint64_t)k * 64 == last) s_last[par] = (uint32_t)raw[k];  // (the low half is the file)
+        __syncthreads();  // (s_wtot[par] and s_last[par] are rewritten two tiles later, after the next barrier)
         uint32_t wbase = 0, ttot = 0;
 #pragma unroll
         for (int ww = 0; ww < kCWaves; ww++) {
-            const uint32_t c = s_wtot[ww];
+            const uint32_t c = s_wtot[par][ww];
             if (ww < w) wbase += c;
             ttot += c;
         }
+        if (tb + kCTile < hi) load_tile(tb + kCTile);
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             if ((keep >> k) & 1u) {
@@ -1322,8 +1336,8 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             }
         }
         o += ttot;
-        __syncthreads();  // bitmap, s_wtot and s_flag users done before the next tile
     }
+    __syncthreads();
     for (int d = threadIdx.x; d < kRadix; d += kCBlock) {
         uint32_t tt = 0;
 #pragma unroll
