@@ -83,8 +83,8 @@ typedef struct {
     /* tokenizer kernel (K1b k_tok_emit), the dominant kernel */
     double emit_ms;        /* duration of the last k_tok_emit launch */
     uint64_t emit_bytes;   /* its algorithmic bytes: B text read + 8 B per record written */
-    double resolve_ms;     /* K1c k_tok_resolve (tokens the emit kernel left unresolved) */
-    uint64_t resolved_tokens; /* tokens K1b handed to K1c (general path, full hot bucket, raced claim) */
+    double resolve_ms;     /* k_long_verify, the exactness pass of hashed (> 12-letter) keys */
+    uint64_t resolved_tokens; /* tokens K1b's fast path left to its K1c tail (general path, full hot bucket, raced claim) */
     double sort0_ms;       /* first token-sort pass: dedup + lexid remap + compaction (k_sort0_compact) */
     uint64_t sort0_bytes;  /* its algorithmic bytes: 8 B per record read + 8 B per kept record written */
     /* ii_map_files only (0 otherwise): host wall time of reading the files and

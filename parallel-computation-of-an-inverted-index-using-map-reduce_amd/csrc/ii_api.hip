@@ -91,7 +91,7 @@ struct ii_ctx {
 
     hipEvent_t ev[8] = {};
     hipEvent_t ev_emit[2] = {};  // around the last (successful) k_tok_emit launch
-    hipEvent_t ev_res[2] = {};   // [1]: after the k_tok_resolve launch that follows k_tok_emit
+    hipEvent_t ev_res[2] = {};   // around the last k_long_verify launch (none: no long tokens)
     hipEvent_t ev_sc[2 * kMaxTimedPasses] = {};
     uint64_t sc_bytes[kMaxTimedPasses] = {0};  // algorithmic bytes of each timed scatter launch
     int n_sc = 0;
@@ -574,15 +574,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
                                                        c->rec_cap, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
-                                                       P_<uint32_t>(c->chunk_files));
+                                                       P_<uint32_t>(c->chunk_files), P_<LongTok>(c->longs),
+                                                       c->long_cap / kLongShards);
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
-        k_tok_resolve<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, fid, chunk_cnt,
-                                                           c->rec_cap, P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), tab,
-                                                           P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                           P_<LongTok>(c->longs), c->long_cap / kLongShards,
-                                                           P_<uint32_t>(c->chunk_files));
         k_long_totals<<<1, 64, 0, c->st>>>(counters);
-        HIPCK(hipEventRecord(c->ev_res[1], c->st));
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
@@ -601,8 +596,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         c->nlong = cnt[C_LONG];
         if (c->nlong) {
             const dim3 g(kLongShards, (uint32_t)std::min<uint64_t>(128, grid_for(cnt[C_LONGMAX])));
+            HIPCK(hipEventRecord(c->ev_res[0], c->st));
             k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->long_cap / kLongShards,
                                                  P_<uint64_t>(c->trep), counters);
+            HIPCK(hipEventRecord(c->ev_res[1], c->st));
             HIPCK(hipGetLastError());
             CK(read_u64(c, counters, cnt, 4));
             if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
@@ -1437,7 +1434,7 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
     s.ms_map = ev_ms(c->ev[0], c->ev[1]);
     if (c->T) {
         s.emit_ms = ev_ms(c->ev_emit[0], c->ev_emit[1]);
-        s.resolve_ms = ev_ms(c->ev_emit[1], c->ev_res[1]);
+        s.resolve_ms = c->nlong ? ev_ms(c->ev_res[0], c->ev_res[1]) : 0.0;
         s.resolved_tokens = c->n_pending;
         s.emit_bytes = c->nbytes + 8 * c->T;  // tokenize = B + r*T, r = 8-byte record
     }

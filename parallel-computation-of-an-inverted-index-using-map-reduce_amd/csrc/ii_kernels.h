@@ -666,8 +666,69 @@ __device__ __forceinline__ uint64_t pend_limit(const uint64_t* chunk_off, uint64
     return cap ? cbase + cap : chunk_off[c + 1];  // dense: chunk_off is the exclusive scan of the counts
 }
 
+// K1c, the chunk's pending tokens (K1b's list), one per lane, run by the
+// chunk's own wave once its rounds are done: general-path tokens
+// (main.c:105-111 with inner punctuation, > 12 letters or > 16 bytes: key
+// from the text) or fast-path misses (full hot bucket, raced claim: key left
+// in the record slot) — full table lookup / insert (table_find), record.
+// Their dependent loads overlap the other waves' rounds (K1b is VALU-bound,
+// this is latency-bound), instead of a kernel of its own.  Tokens of more
+// than 12 letters (hashed keys) are queued for k_long_verify.
+template <bool kSlow>
+__device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t c,
+                                                const uint64_t* __restrict__ file_start,
+                                                const uint32_t* __restrict__ file_id, uint32_t f_lo, uint32_t f_hi,
+                                                uint32_t fid0, uint64_t cbase, uint64_t cap, uint32_t rot,
+                                                uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
+                                                const Table& tab, uint64_t* __restrict__ rec, uint32_t* hist,
+                                                LongTok* __restrict__ longs, uint64_t long_per) {
+    const int l = lane_id();
+    const uint64_t chunk_lo = c * kChunk;
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + l;
+        bool is_long = false;
+        uint64_t pos = 0, slot = 0;
+        if (i < n) {
+            const uint32_t e = kSlow ? pend[pend_end - 1 - i] : pend[cbase + i];
+            pos = chunk_lo + (e & 0xFFFFu);
+            const uint64_t r = rec_slot(cbase, cap, rot, e >> 16);
+            uint64_t key;
+            if (kSlow) {
+                const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
+                atomicAdd(&hist[k.first], 1u);
+                key = k.key;
+                is_long = k.nlet > 12;
+            } else {
+                key = rec[r];
+            }
+            slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
+            const uint32_t f = f_lo == f_hi ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
+            rec[r] = (slot << 32) | f;
+        }
+        if (!kSlow) continue;
+        // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
+        const uint64_t lm = __ballot(is_long);
+        if (lm) {
+            const uint32_t shard = (uint32_t)(c & (kLongShards - 1));
+            const int leader = __builtin_ctzll(lm);
+            unsigned long long base = 0;
+            if (l == leader)
+                base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard], (unsigned long long)__popcll(lm));
+            base = (unsigned long long)__shfl((long long)base, leader, 64);
+            if (is_long) {
+                const uint64_t g = base + (uint64_t)__popcll(lm & lt);
+                if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
+                else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
+            }
+        }
+    }
+}
+
 // kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
-// bit 0 = skip the table probe, bit 2 = skip the letter histogram.
+// bit 0 = skip the table probe, bit 2 = skip the letter histogram, bit 3 =
+// skip the per-token step (classify, scan and list only), bit 4 = skip the
+// pending tokens (K1c).
 template <int kAblate = 0>
 __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                      const uint64_t* __restrict__ file_start,
@@ -675,7 +736,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                      uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
-                                                     const uint32_t* __restrict__ cf) {
+                                                     const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
+                                                     uint64_t long_per) {
     __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
     const uint64_t c = wave_chunk();
     if (c >= nch) return;
@@ -731,6 +793,10 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             for (uint32_t m = kept[1]; m; m &= m - 1) W.off[o++] = (uint16_t)(16 * (64 + l) + __builtin_ctz(m));
         }
         wave_sync();
+        if (kAblate & 8) {  // rounds without the per-token step
+            out += ntok;
+            continue;
+        }
         const uint32_t pbase = (uint32_t)(lo - chunk_lo);
         // 3. keys + cooperative hot-bucket probes, one token per lane (issuing
         //    the next batch's probes before resolving this one measured slower:
@@ -778,93 +844,22 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
         }
         out += ntok;
     }
+    // 4. K1c: the chunk's pending tokens.  The lanes read entries other lanes
+    //    of this wave stored: the stores are complete (vmcnt) before the loads.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (!(kAblate & 16)) {
+        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, cap, rot, pend_end, pend,
+                               npf, tab, rec, W.hist, longs, long_per);
+        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, cap, rot, pend_end, pend,
+                              nps, tab, rec, W.hist, longs, long_per);
+    }
     wave_sync();
     if (l < 26) chunk_hist[c * 26 + l] = W.hist[l];
     if (l == 0) {
         pend_cnt[c] = npf | (nps << 16);
         if (cap) chunk_off[c] = out;  // fixed-capacity layout: the chunk's token count
     }
-}
-
-// K1c: the tokens K1b left unresolved, one per lane, one wave per chunk —
-// general-path tokens (main.c:105-111 with inner punctuation, > 12 letters or
-// > 16 bytes: key from the text in HBM) and words whose hot bucket is full or
-// whose claim raced — full table lookup / insert (table_find), record.  Many
-// independent lookups in flight instead of a phase inside K1b.  Tokens of
-// more than 12 letters (hashed keys) are queued for k_long_verify.
-__global__ __launch_bounds__(kBlock) void k_tok_resolve(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
-                                                        const uint64_t* __restrict__ file_start,
-                                                        const uint32_t* __restrict__ file_id,
-                                                        const uint64_t* __restrict__ chunk_off, uint64_t cap,
-                                                        const uint32_t* __restrict__ pend,
-                                                        const uint32_t* __restrict__ pend_cnt, Table tab,
-                                                        uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                        LongTok* __restrict__ longs, uint64_t long_per,
-                                                        const uint32_t* __restrict__ cf) {
-    __shared__ uint32_t s_hist[kWG][32];
-    const uint64_t c = wave_chunk();
-    if (c >= nch) return;
-    const uint32_t pc = pend_cnt[c];
-    if (pc == 0) return;
-    const int l = lane_id();
-    uint32_t* hist = s_hist[c - (uint64_t)blockIdx.x * kWG];
-    if (l < 32) hist[l] = 0;
-    wave_sync();
-    const uint64_t chunk_lo = c * kChunk;
-    const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
-    const bool fsame = f_lo == f_hi;
-    const uint64_t cbase = chunk_base(chunk_off, cap, c);
-    const uint64_t pend_end = pend_limit(chunk_off, cap, cbase, c);
-    const uint32_t rot = chunk_rot(c);
-    const uint64_t lt = lanemask_lt();
-    // kSlow: general-path tokens (key from the text); else fast-path misses (key in the record slot)
-    auto resolve = [&](auto slow_tag, uint32_t n) {
-        constexpr bool kSlow = decltype(slow_tag)::value;
-        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + l;
-            bool is_long = false;
-            uint64_t pos = 0, slot = 0;
-            if (i < n) {
-                const uint32_t e = kSlow ? pend[pend_end - 1 - i] : pend[cbase + i];
-                pos = chunk_lo + (e & 0xFFFFu);
-                const uint64_t r = rec_slot(cbase, cap, rot, e >> 16);
-                uint64_t key;
-                if (kSlow) {
-                    const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0,
-                                                 tab.seed, 0);
-                    atomicAdd(&hist[k.first], 1u);
-                    key = k.key;
-                    is_long = k.nlet > 12;
-                } else {
-                    key = rec[r];
-                }
-                slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
-                rec[r] = (slot << 32) | f;
-            }
-            if (!kSlow) continue;
-            // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
-            const uint64_t lm = __ballot(is_long);
-            if (lm) {
-                const uint32_t shard = (uint32_t)(c & (kLongShards - 1));
-                const int leader = __builtin_ctzll(lm);
-                unsigned long long base = 0;
-                if (l == leader)
-                    base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard],
-                                     (unsigned long long)__popcll(lm));
-                base = (unsigned long long)__shfl((long long)base, leader, 64);
-                if (is_long) {
-                    const uint64_t g = base + (uint64_t)__popcll(lm & lt);
-                    if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
-                    else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
-                }
-            }
-        }
-    };
-    resolve(std::false_type{}, pc & 0xFFFFu);
-    resolve(std::true_type{}, pc >> 16);
-    wave_sync();
-    if (l < 26 && hist[l]) chunk_hist[c * 26 + l] += hist[l];
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)

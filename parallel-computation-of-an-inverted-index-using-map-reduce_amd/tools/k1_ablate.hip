@@ -1,7 +1,8 @@
 // k1_ablate.hip — timing experiment for the K1 emit kernel (not product code).
 // Times k_tok_emit<kAblate> variants on one synthetic Zipf corpus:
-//   0 full, 1 no table probe, 4 no letter histogram, 5 neither; and
-//   k_tok_count.  The K1c resolve kernel is timed after each emit run.
+//   0 full, 16 without the K1c tail (pending tokens), 1 no table probe,
+//   4 no letter histogram, 5 neither, 8 no per-token step (classify + scan +
+//   token list only); and k_tok_count and a read-only pass.
 // Usage: k1_ablate [bytes] [files] [vocab]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -16,7 +17,6 @@ extern "C" int iigen_fill(const iigen_params*, const uint64_t*, uint8_t*, int);
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-static float g_res;  // K1c time of the fastest emit run
 // read-only reference: the count kernel's access pattern (one wave per
 // chunk, 16 B per lane, 8 loads in flight), XOR of the words
 __global__ __launch_bounds__(kBlock) void k_read_only(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
@@ -52,8 +52,8 @@ template <int A>
 float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, uint32_t nf, uint64_t* chunk_off,
           Table tab, uint64_t nslots, uint64_t* rec, uint32_t* chist, LongTok* longs, uint64_t lcap, uint64_t nch,
           uint32_t* pend, uint32_t* pcnt) {
-    hipEvent_t a, b, c;
-    CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); CK(hipEventCreate(&c));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     uint32_t* cf;
     const uint32_t wg = (uint32_t)((nch + kWG - 1) / kWG);
     CK(hipMalloc(&cf, 12 * nch));
@@ -63,13 +63,12 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
         CK(hipMemset(tab.keys, 0, nslots * 8));
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
-        k_tok_emit<A><<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, tab, rec, chist, pend, pcnt, cf);
+        k_tok_emit<A><<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, tab, rec, chist, pend, pcnt, cf,
+                                      longs, lcap / kLongShards);
         CK(hipEventRecord(b));
-        k_tok_resolve<<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, pend, pcnt, tab, rec, chist, longs, lcap / kLongShards, cf);
-        CK(hipEventRecord(c));
-        CK(hipEventSynchronize(c));
-        float ms, ms2; CK(hipEventElapsedTime(&ms, a, b)); CK(hipEventElapsedTime(&ms2, b, c));
-        if (ms < best) { best = ms; g_res = ms2; }
+        CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
     }
     return best;
 }
@@ -112,9 +111,9 @@ int main(int argc, char** argv) {
 #define RUN(A) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt); \
     unsigned long long np_ = 0; std::vector<uint32_t> pc_(nch); CK(hipMemcpy(pc_.data(), pcnt, 4 * nch, hipMemcpyDeviceToHost)); \
     for (auto x : pc_) np_ += (x & 0xFFFFu) + (x >> 16); \
-    printf("emit ablate %2d: %.3f ms  resolve %.3f ms  pending %llu\n", A, e_, g_res, np_); } while (0)
+    printf("emit ablate %2d: %.3f ms  pending %llu\n", A, e_, np_); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
-    RUN(0); RUN(1); RUN(4); RUN(5);
+    RUN(0); RUN(16); RUN(1); RUN(4); RUN(5); RUN(8);
     printf("count (best of 5): %.3f ms\n", best_of([&] { k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
     printf("read-only (best of 5): %.3f ms\n", best_of([&] { k_read_only<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
     return 0;
