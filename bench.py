@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--vocab", type=int, default=None)
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--cpu-baseline", choices=["quick", "none"], default="quick")
+    p.add_argument("--cpu-slice-kb", type=int, default=25,
+                   help="file size of the reference's 360-file slice (BASELINE.md's protocol: 1000)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--gen-threads", type=int, default=16)
@@ -177,10 +179,11 @@ def write_files(text, off, nf, td):
 
 
 def cpu_baseline(a, text, off, runs=5):
-    """CPU baseline, bounded to about a minute:
-    the reference itself (oracle/_ref/tema1 = gcc -O2 main.c) on a
+    """CPU baseline, bounded to about a minute by
+    default: the reference itself (oracle/_ref/tema1 = gcc -O2 main.c) on a
     reference-feasible slice of the same generator — 360 files (its MAX_FILES,
-    main.c:8) of 25 KB — at M = cores / R = 26 and M = R = cores, median of
+    main.c:8) of --cpu-slice-kb KB (25; BASELINE.md's protocol slice is 1000,
+    minutes per run) — at M = cores / R = 26 and M = R = cores, median of
     `runs` each; its as-shipped ASan build (Makefile:2) once for context; and
     the multithreaded hash-based restatement (oracle ii_oracle_index_mt,
     bit-exact) over the WHOLE corpus with `cores` threads.
@@ -190,7 +193,7 @@ def cpu_baseline(a, text, off, runs=5):
     ref = os.path.join(REPO, "oracle", "_ref", "tema1")
     asan = os.path.join(REPO, "oracle", "_ref", "tema1_asan")
     out = {"unit": "GB/s", "cores": cores, "host_cpus": os.cpu_count()}
-    sl_files, sl_bytes = 360, 360 * 25_000
+    sl_files, sl_bytes = 360, 360 * 1000 * a.cpu_slice_kb
     st, so = ii_ctypes.zipf_corpus(sl_bytes, sl_files, a.vocab, a.seed + 77, threads=min(8, cores))
     m_ok = safe_mappers([int(so[f + 1] - so[f]) for f in range(sl_files)], cores)
     lanes = []
@@ -201,8 +204,19 @@ def cpu_baseline(a, text, off, runs=5):
 
             def timed(binary, M, R):
                 t0 = time.perf_counter()
-                subprocess.run([binary, str(M), str(R), "list.txt"], cwd=td, check=True, stdout=subprocess.DEVNULL,
-                               stderr=subprocess.DEVNULL, timeout=600)
+                pr = subprocess.Popen([binary, str(M), str(R), "list.txt"], cwd=td, stdout=subprocess.DEVNULL,
+                                      stderr=subprocess.DEVNULL)
+                while True:  # a progress line every 30 s (a long slice is not a hang)
+                    try:
+                        rc = pr.wait(timeout=30)
+                        break
+                    except subprocess.TimeoutExpired:
+                        log("cpu baseline: %s still running (%.0f s)" % (os.path.basename(binary), time.perf_counter() - t0))
+                        if time.perf_counter() - t0 > 1800:
+                            pr.kill()
+                            raise
+                if rc != 0:
+                    raise subprocess.CalledProcessError(rc, binary)
                 return time.perf_counter() - t0
 
             for M, R in [(m_ok, 26), (m_ok, m_ok)]:
@@ -220,8 +234,8 @@ def cpu_baseline(a, text, off, runs=5):
             shutil.rmtree(td, ignore_errors=True)
         best = max(lanes[:2], key=lambda x: x["GBps"])
         out.update({"value": best["GBps"], "kind": "reference", "M": best["M"], "R": best["R"],
-                    "sample": "reference binary on 360 files x 25 KB (%.1f MB) of the same generator (vocab %d); "
-                              "median of %d" % (sl_bytes / 1e6, a.vocab, runs), "reference_lanes": lanes})
+                    "sample": "reference binary on 360 files x %d KB (%.1f MB) of the same generator (vocab %d); "
+                              "median of %d" % (a.cpu_slice_kb, sl_bytes / 1e6, a.vocab, runs), "reference_lanes": lanes})
     # the bit-exact multithreaded restatement at full size
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_py import oracle_index

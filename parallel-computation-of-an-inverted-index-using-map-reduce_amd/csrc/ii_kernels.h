@@ -113,11 +113,11 @@ __device__ __forceinline__ unsigned long long table_claim(const Table& t, uint64
 // did not hold the key): the 8-slot hot bucket (one 64-B line) and the word's
 // big-table home slot are loaded together, so a word living at its big-table
 // home costs one round trip; the bucket is scanned with bit masks in probe
-// order (home, home+1, ... within the bucket); a full bucket sends the word
-// to the big table (linear probing).
+// order (from the first slot of the home slot's pair, wrapping inside the
+// bucket); a full bucket sends the word to the big table (linear probing).
 __device__ __forceinline__ uint32_t table_find(const Table& t, uint64_t key, uint32_t home, uint64_t pos) {
-    const uint32_t h7 = home & (kBucket - 1);
-    const uint64_t bbase = home - h7;
+    const uint32_t h7 = home & (kBucket - 2);  // probe order: from the home slot's pair
+    const uint64_t bbase = home & ~(uint32_t)(kBucket - 1);
     uint64_t h = big_home(t, key);
     const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(t.keys + bbase);
     const ulonglong2 p0 = bp[0], p1 = bp[1], p2 = bp[2], p3 = bp[3];
@@ -373,36 +373,6 @@ __device__ __forceinline__ uint32_t byte_dyn(const uint4& b, uint32_t j) {
     return (sel4(j >> 2, b.x, b.y, b.z, b.w) >> (8 * (j & 3u))) & 0xFFu;
 }
 
-// General form of the cleaning loop (main.c:105-111): 16 bytes per step,
-// SWAR classes, then only the letter bytes are visited.  Stops at whitespace,
-// NUL or the 299th letter.  first16 = the token's first 16 bytes.
-__device__ __forceinline__ TokKey general_key(uint4 b, const uint8_t* s_text, const uint8_t* __restrict__ text,
-                                              uint64_t nbytes, uint64_t tile_lo, uint32_t p, uint64_t seed, uint32_t lim) {
-    uint64_t packed = 0, hash = 1469598103934665603ull;
-    uint32_t n = 0, first = 0;
-    for (;;) {
-        const Classes cl = classify16(b);
-        const uint32_t term = cl.ws | cl.nul;
-        const uint32_t e = term ? __builtin_ctz(term) : 16u;
-        bool done = term != 0;
-        for (uint32_t m = cl.letter & ((1u << e) - 1u); m; m &= m - 1) {
-            const uint32_t lc = (byte_dyn(b, __builtin_ctz(m)) | 0x20u) - 0x61u;
-            if (n == 0) first = lc;
-            n++;
-            if (n <= 12) packed |= (uint64_t)(lc + 1) << (64 - 5 * n);
-            hash = (hash ^ (lc + 1)) * 1099511628211ull;
-            if (n == (uint32_t)kMaxWord) {
-                done = true;
-                break;
-            }
-        }
-        if (done) break;
-        p += 16;
-        b = tile_block16(s_text, text, nbytes, tile_lo, p, lim);
-    }
-    return TokKey{n <= 12 ? packed : long_key(hash, n, seed), n, first};
-}
-
 // ---------------------------------------------------------------- K1 chunks
 // The text is cut into chunks of kChunk bytes, ONE WAVE per chunk (kWG
 // chunks per workgroup): a wave walks its chunk alone, with wave-level
@@ -504,9 +474,12 @@ __device__ __forceinline__ uint32_t chunk_rot(uint64_t c) {
 __device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap, uint64_t c) {
     return cap ? c * cap : chunk_off[c];
 }
-// index of the chunk's j-th record (cbase from chunk_base, rot = chunk_rot(c))
-__device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint64_t cap, uint32_t rot, uint32_t j) {
-    return cap ? cbase + ((j + rot) & (uint32_t)(kChunkCap - 1)) : cbase + j;
+// index of the chunk's j-th record: cbase from chunk_base, (rot, wrap) =
+// (chunk_rot(c), kChunkCap - 1) in the fixed-capacity layout, (0, ~0) dense
+__device__ __forceinline__ uint32_t rec_wrap(uint64_t cap) { return cap ? (uint32_t)(kChunkCap - 1) : ~0u; }
+__device__ __forceinline__ uint32_t rec_rot(uint64_t cap, uint64_t c) { return cap ? chunk_rot(c) : 0u; }
+__device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint32_t wrap, uint32_t rot, uint32_t j) {
+    return cbase + ((j + rot) & wrap);
 }
 
 // ---------------------------------------------------------------- K1b emit
@@ -549,21 +522,47 @@ struct RoundRegs {
     uint4 v[kWin];  // lane's windows
     uint4 h;        // left piece (lane 0) / halo pieces (lanes 1..kHaloPieces)
 };
+// A round's loads are plain 16-B loads of aligned blocks with no branch
+// between an interior and an edge form (two forms merge into one set of
+// registers only by waiting for the loads): a block that starts past the
+// text's last block is loaded from that block, and one before the text from
+// block 0; store_round replaces what lies outside [0, nbytes) by spaces.  So
+// the next round's loads stay in flight while this round is worked on.
+__device__ __forceinline__ int64_t piece_pos(uint64_t lo, int l) {  // left piece (lane 0) / halo pieces
+    return (int64_t)lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1);
+}
 __device__ __forceinline__ void fetch_round(RoundRegs& r, const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t lo) {
     const int l = lane_id();
-    r.h = make_uint4(0, 0, 0, 0);
-    if (lo >= 16 && lo + kRoundStaged <= nbytes) {  // (wave-uniform) every piece lies inside the text: plain loads
+    const uint64_t last = (nbytes - 1) & ~15ull;
 #pragma unroll
-        for (int j = 0; j < kWin; j++) r.v[j] = *reinterpret_cast<const uint4*>(text + lo + 16 * (64 * j + l));
-        if (l <= kHaloPieces) r.h = *reinterpret_cast<const uint4*>(text + lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1));
-        return;
+    for (int j = 0; j < kWin; j++) {
+        const uint64_t g = lo + 16 * (64 * j + l);
+        r.v[j] = *reinterpret_cast<const uint4*>(text + (g < last ? g : last));
     }
-#pragma unroll
-    for (int j = 0; j < kWin; j++) r.v[j] = load16(text, nbytes, (int64_t)lo + 16 * (64 * j + l));
-    if (l <= kHaloPieces) r.h = load16(text, nbytes, (int64_t)lo + 16 * (l == 0 ? -1 : kRoundWins + l - 1));
+    r.h = make_uint4(0, 0, 0, 0);
+    if (l <= kHaloPieces) {
+        const int64_t g = piece_pos(lo, l);
+        r.h = *reinterpret_cast<const uint4*>(text + (g < 0 ? 0 : (uint64_t)g < last ? (uint64_t)g : last));
+    }
 }
-__device__ __forceinline__ void store_round(uint8_t* s_text, const RoundRegs& r) {
+__device__ __forceinline__ uint4 outside_spaces(uint4 v, int64_t g, uint64_t nbytes) {
+    if (g < 0 || (uint64_t)g >= nbytes) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    const int64_t left = (int64_t)(nbytes - (uint64_t)g);
+    if (left < 16) {
+        v.x = keep_bytes(v.x, left);
+        v.y = keep_bytes(v.y, left - 4);
+        v.z = keep_bytes(v.z, left - 8);
+        v.w = keep_bytes(v.w, left - 12);
+    }
+    return v;
+}
+__device__ __forceinline__ void store_round(uint8_t* s_text, RoundRegs r, uint64_t nbytes, uint64_t lo) {
     const int l = lane_id();
+    if (lo < 16 || lo + kRoundStaged > nbytes) {  // (wave-uniform) a piece may lie outside the text
+#pragma unroll
+        for (int j = 0; j < kWin; j++) r.v[j] = outside_spaces(r.v[j], (int64_t)(lo + 16 * (64 * j + l)), nbytes);
+        r.h = outside_spaces(r.h, piece_pos(lo, l), nbytes);
+    }
 #pragma unroll
     for (int j = 0; j < kWin; j++) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (64 * j + l)) = r.v[j];
     if (l <= kHaloPieces) *reinterpret_cast<uint4*>(s_text + 16 + 16 * (l == 0 ? -1 : kRoundWins + l - 1)) = r.h;
@@ -577,17 +576,13 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x) {
     return (r & 0x3FFu) | ((r >> 6) & 0xFFC00u);                // b0@15 b1@10 b2@5 b3@0
 }
 
-// Byte g (0..15) of the 16-byte value x[0..3] removed: the bytes above it
-// move down one place.
-__device__ __forceinline__ void drop_byte(uint32_t (&x)[4], uint32_t g) {
-    const uint32_t s[4] = {__builtin_amdgcn_alignbyte(x[1], x[0], 1), __builtin_amdgcn_alignbyte(x[2], x[1], 1),
-                           __builtin_amdgcn_alignbyte(x[3], x[2], 1), x[3] >> 8};
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int kb = (int)g - 4 * i;  // bytes of dword i that stay
-        const uint32_t m = kb >= 4 ? 0xFFFFFFFFu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1u;
-        x[i] = (x[i] & m) | (s[i] & ~m);
-    }
+// Byte g (0..15) of the 16-byte value lo | hi << 64 removed: the bytes above
+// it move down one place (three 64-bit shifts and two masked merges).
+__device__ __forceinline__ void drop_byte(uint64_t& lo, uint64_t& hi, uint32_t g) {
+    const uint64_t ml = g >= 8 ? ~0ull : (1ull << (8 * g)) - 1ull;         // bytes of lo that stay
+    const uint64_t mh = g < 8 ? 0ull : (1ull << (8 * (g - 8))) - 1ull;     // bytes of hi that stay
+    lo = (lo & ml) | (((lo >> 8) | (hi << 56)) & ~ml);
+    hi = (hi & mh) | ((hi >> 8) & ~mh);
 }
 
 // Register key path of the cleaning loop (main.c:105-111): the token ends
@@ -610,18 +605,24 @@ __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint
     if (n == 0 || n > 12) return false;
     const uint32_t a = 16u + p, al = a & 3u;
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_text) + (a >> 2);
-    const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2], d3 = s32[3], d4 = s32[4];
-    uint32_t x[4] = {__builtin_amdgcn_alignbyte(d1, d0, al), __builtin_amdgcn_alignbyte(d2, d1, al),
-                     __builtin_amdgcn_alignbyte(d3, d2, al), __builtin_amdgcn_alignbyte(d4, d3, al)};
+    const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2], d3 = s32[3];
+    uint32_t x[3] = {__builtin_amdgcn_alignbyte(d1, d0, al), __builtin_amdgcn_alignbyte(d2, d1, al),
+                     __builtin_amdgcn_alignbyte(d3, d2, al)};
     if (lm != (1u << n) - 1u) {  // other bytes before or among the letters
         if (e > 16) return false;
         uint32_t gaps = ~lm & ((2u << (31 - __builtin_clz(lm))) - 1u);  // below the last letter
         if (__popc(gaps) > 3) return false;
+        const uint32_t d4 = s32[4];
+        uint64_t lo = ((uint64_t)x[1] << 32) | x[0];
+        uint64_t hi = ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, al) << 32) | x[2];
         while (gaps) {  // from the highest down: the lower positions stay put
             const uint32_t g = 31 - __builtin_clz(gaps);
-            drop_byte(x, g);
+            drop_byte(lo, hi, g);
             gaps &= ~(1u << g);
         }
+        x[0] = (uint32_t)lo;
+        x[1] = (uint32_t)(lo >> 32);
+        x[2] = (uint32_t)hi;
     }
     const uint64_t key = ((uint64_t)pack4(x[0]) << 44) | ((uint64_t)pack4(x[1]) << 24) | ((uint64_t)pack4(x[2]) << 4);
     k.key = key & (~0ull << (64 - 5 * n));
@@ -632,27 +633,23 @@ __device__ __forceinline__ bool round_fast_key(const uint8_t* s_text, const uint
 
 // Hot-table probe of K1b: a lane loads the two 16-B slot pairs that begin
 // its key's probe order in the 8-slot bucket (home's pair and the next, one
-// 64-B line).  A frequent word sits at or next to its home slot (it was
-// inserted while its bucket was still empty), so the short window decides
+// 64-B line; the probe order of a bucket starts at the home slot's pair, see
+// table_find).  A frequent word sits in its home pair or the next one (it
+// was inserted while its bucket was still empty), so the short window decides
 // almost every token; the rest go to K1c.  (Two lanes sharing one token's
 // loads, so that an instruction touches half as many lines, measured 0.35 ms
 // slower at 10 GB: the shuffles that route keys and results cost more VALU.)
-__device__ __forceinline__ uint32_t rotr8(uint32_t x, uint32_t s) { return ((x >> s) | (x << (8 - s))) & 0xFFu; }
-// Lookup from a partly seen bucket: a match is the slot; otherwise the first
-// empty slot inside the seen prefix of the probe order is claimed
-// (table_find's rule, so a word still lives in exactly one place); a seen
-// prefix with no empty slot, or a raced claim, leaves the word to K1c.
-__device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t match, uint32_t full, uint32_t known,
-                                                   uint64_t key, uint32_t home, uint64_t pos) {
-    const uint32_t h7 = home & (kBucket - 1);
-    const uint32_t bbase = home - h7;
-    if (match) return bbase + __builtin_ctz(match);
-    const uint32_t kr = rotr8(known, h7);
-    const uint32_t prefix = kr & ~(kr + 1u);  // probe positions 0.. seen without a gap
-    const uint32_t er = rotr8(~full & 0xFFu, h7) & prefix;
-    if (!er) return kSlotNone;
-    const uint32_t p = (h7 + __builtin_ctz(er)) & (kBucket - 1);
-    return table_claim(t, bbase + p, key, pos) == key ? bbase + p : kSlotNone;
+// match / empty: 4-bit masks over the seen probe positions 0..3.  A match is
+// the slot; otherwise the first empty position is claimed (table_find's rule,
+// so a word still lives in exactly one place); no empty slot, or a raced
+// claim, leaves the word to K1c.
+__device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t match, uint32_t empty, uint64_t key,
+                                                   uint32_t bbase, uint32_t start, uint64_t pos) {
+    const uint32_t m = match ? match : empty;
+    if (!m) return kSlotNone;
+    const uint32_t s = bbase + ((start + __builtin_ctz(m)) & (kBucket - 1));
+    if (match) return s;
+    return table_claim(t, s, key, pos) == key ? s : kSlotNone;
 }
 
 // Unresolved token of a chunk (K1b -> K1c), one u32: chunk-relative start
@@ -664,6 +661,87 @@ __device__ __forceinline__ uint32_t bucket_resolve(const Table& t, uint32_t matc
 static_assert(kChunk <= 65536 && kChunkCap <= 32768, "pending-token fields");
 __device__ __forceinline__ uint64_t pend_limit(const uint64_t* chunk_off, uint64_t cap, uint64_t cbase, uint64_t c) {
     return cap ? cbase + cap : chunk_off[c + 1];  // dense: chunk_off is the exclusive scan of the counts
+}
+
+// General form of the cleaning loop (main.c:105-111) for the token at text
+// position pos, one aligned 16-byte block per step (SWAR classes; the bytes
+// of the first block before pos are ignored).  The cleaned word's letters
+// form a stream of codes (1..26, one byte each) that is hashed one dword (4
+// letters) at a time; the first three dwords are the first 12 letters (the
+// exact key of a word of <= 12 letters).  A block whose letters form one run
+// (a plain or capitalised word, trailing punctuation) is appended as a whole;
+// other blocks letter by letter.  Stops at whitespace, NUL or the 299th letter.
+struct LetterStream {
+    uint64_t hash;
+    uint32_t pend, pc;  // codes not yet folded: pc bytes (0..3)
+    uint32_t nd, n;     // dwords folded, letters
+    uint32_t d0, d1, d2;
+    __device__ __forceinline__ void fold(uint32_t w) {
+        d0 = nd == 0 ? w : d0;
+        d1 = nd == 1 ? w : d1;
+        d2 = nd == 2 ? w : d2;
+        hash = (hash ^ w) * 1099511628211ull;
+        nd++;
+    }
+};
+__device__ __forceinline__ TokKey general_key(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t pos,
+                                              uint64_t seed) {
+    LetterStream st{1469598103934665603ull ^ seed, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    uint64_t g = pos & ~15ull;
+    uint32_t below = (1u << (pos & 15u)) - 1u;  // first block: bytes before the token
+    for (;;) {
+        const uint4 b = load16(text, nbytes, (int64_t)g);
+        const Classes cl = classify16(b);
+        const uint32_t term = (cl.ws | cl.nul) & ~below;
+        const uint32_t e = term ? __builtin_ctz(term) : 16u;
+        const uint32_t lm = cl.letter & ~below & ((1u << e) - 1u);
+        below = 0;
+        const uint32_t k = __popc(lm);
+        if (lm && (lm & (lm + (lm & (0u - lm)))) == 0 && st.n + k <= (uint32_t)kMaxWord) {
+            // one run of k letters from byte s: shift it to byte 0, letter codes, bytes >= k cleared
+            const uint32_t s = __builtin_ctz(lm);
+            uint64_t lo = ((uint64_t)b.y << 32) | b.x, hi = ((uint64_t)b.w << 32) | b.z;
+            if (s >= 8) {
+                lo = hi >> (8 * (s - 8));
+                hi = 0;
+            } else if (s) {
+                lo = (lo >> (8 * s)) | (hi << (64 - 8 * s));
+                hi >>= 8 * s;
+            }
+            lo &= (k >= 8 ? ~0ull : (1ull << (8 * k)) - 1ull) & 0x1F1F1F1F1F1F1F1Full;
+            hi &= (k <= 8 ? 0ull : k >= 16 ? ~0ull : (1ull << (8 * (k - 8))) - 1ull) & 0x1F1F1F1F1F1F1F1Full;
+            // behind the pending codes: 5 dwords, the first (pc + k) / 4 of them complete
+            const uint32_t sh = 8 * st.pc;
+            const uint32_t w[5] = {st.pend | ((uint32_t)lo << sh), (uint32_t)(lo >> (32 - sh)),
+                                   (uint32_t)(((hi << 32) | (lo >> 32)) >> (32 - sh)), (uint32_t)(hi >> (32 - sh)),
+                                   (uint32_t)((hi >> 32) >> (32 - sh))};
+            const uint32_t t = st.pc + k, full = t >> 2;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if ((uint32_t)i < full) st.fold(w[i]);
+            st.pend = sel4(full & 3u, w[0], w[1], w[2], w[3]);
+            st.pend = full == 4 ? w[4] : st.pend;
+            st.pc = t & 3u;
+            st.n += k;
+        } else {
+            for (uint32_t m = lm; m && st.n < (uint32_t)kMaxWord; m &= m - 1) {
+                st.pend |= (byte_dyn(b, __builtin_ctz(m)) & 0x1Fu) << (8 * st.pc);
+                st.n++;
+                if (++st.pc == 4) {
+                    st.fold(st.pend);
+                    st.pend = 0;
+                    st.pc = 0;
+                }
+            }
+        }
+        if (term || st.n == (uint32_t)kMaxWord) break;
+        g += 16;
+    }
+    if (st.pc) st.fold(st.pend);
+    const uint64_t key = st.n <= 12 ? ((uint64_t)pack4(st.d0) << 44) | ((uint64_t)pack4(st.d1) << 24) |
+                                          ((uint64_t)pack4(st.d2) << 4)
+                                    : long_key(st.hash, st.n, seed);
+    return TokKey{key, st.n, st.n ? (st.d0 & 31u) - 1u : 0u};
 }
 
 // K1c, the chunk's pending tokens (K1b's list), one per lane, run by the
@@ -678,13 +756,12 @@ template <bool kSlow>
 __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t c,
                                                 const uint64_t* __restrict__ file_start,
                                                 const uint32_t* __restrict__ file_id, uint32_t f_lo, uint32_t f_hi,
-                                                uint32_t fid0, uint64_t cbase, uint64_t cap, uint32_t rot,
+                                                uint32_t fid0, uint64_t cbase, uint32_t wrap, uint32_t rot,
                                                 uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
                                                 const Table& tab, uint64_t* __restrict__ rec, uint32_t* hist,
                                                 LongTok* __restrict__ longs, uint64_t long_per) {
     const int l = lane_id();
     const uint64_t chunk_lo = c * kChunk;
-    const uint64_t lt = lanemask_lt();
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + l;
         bool is_long = false;
@@ -692,10 +769,10 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
         if (i < n) {
             const uint32_t e = kSlow ? pend[pend_end - 1 - i] : pend[cbase + i];
             pos = chunk_lo + (e & 0xFFFFu);
-            const uint64_t r = rec_slot(cbase, cap, rot, e >> 16);
+            const uint64_t r = rec_slot(cbase, wrap, rot, e >> 16);
             uint64_t key;
             if (kSlow) {
-                const TokKey k = general_key(global_block16(text, nbytes, pos), nullptr, text, nbytes, pos, 0, tab.seed, 0);
+                const TokKey k = general_key(text, nbytes, pos, tab.seed);
                 atomicAdd(&hist[k.first], 1u);
                 key = k.key;
                 is_long = k.nlet > 12;
@@ -717,7 +794,7 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                 base = atomicAdd((unsigned long long*)&tab.counters[C_LSHARD + 16 * shard], (unsigned long long)__popcll(lm));
             base = (unsigned long long)__shfl((long long)base, leader, 64);
             if (is_long) {
-                const uint64_t g = base + (uint64_t)__popcll(lm & lt);
+                const uint64_t g = base + lanes_below(lm);
                 if (g < long_per) longs[shard * long_per + g] = LongTok{pos, slot};
                 else atomicOr((unsigned long long*)&tab.counters[C_OVERFLOW], 2ull);
             }
@@ -749,8 +826,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
     const bool fsame = f_lo == f_hi;
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
-    const uint32_t rot = chunk_rot(c);
-    const uint64_t lt = lanemask_lt();
+    const uint32_t rot = rec_rot(cap, c), wrap = rec_wrap(cap);
     uint32_t out = 0;               // records emitted so far (wave-uniform)
     uint32_t npf = 0, nps = 0;      // tokens left to K1c: fast-path misses, general-path tokens
     const uint64_t pend_end = pend_limit(chunk_off, cap, cbase, c);
@@ -759,8 +835,10 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     fetch_round(nxt, text, nbytes, chunk_lo);
     for (uint64_t lo = chunk_lo; lo < chunk_hi; lo += kRound) {
         wave_sync();  // the previous round's readers of W are done
-        store_round(W.text, nxt);
-        if (lo + kRound < chunk_hi) fetch_round(nxt, text, nbytes, lo + kRound);
+        store_round(W.text, nxt, nbytes, lo);
+        // the next round (the last round re-loads its own blocks, cache hits: a
+        // conditional fetch would merge registers and wait for the loads here)
+        fetch_round(nxt, text, nbytes, lo + kRound < chunk_hi ? lo + kRound : lo);
         wave_sync();
         // 1. kept starts and window masks (windows re-read from LDS: the next
         //    round's bytes are in flight in the registers)
@@ -813,19 +891,23 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             if (kAblate & 1) {
                 if (fast) slot = home;
             } else {
-                // the two 16-B slot pairs that begin the key's probe order in its 8-slot bucket (home's
-                // pair and the next; one 64-B line); a lane without a key probes key 0's bucket, harmlessly
-                const uint32_t h7 = home & (kBucket - 1), bbase = home - h7, p0 = h7 >> 1, p1 = (p0 + 1) & 3u;
-                const ulonglong2 qa = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + 2 * p0);
-                const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + 2 * p1);
-                const uint32_t match = ((uint32_t)(qa.x == tk.key) << (2 * p0)) | ((uint32_t)(qa.y == tk.key) << (2 * p0 + 1)) |
-                                       ((uint32_t)(qb.x == tk.key) << (2 * p1)) | ((uint32_t)(qb.y == tk.key) << (2 * p1 + 1));
-                const uint32_t full = ((uint32_t)(qa.x != 0ull) << (2 * p0)) | ((uint32_t)(qa.y != 0ull) << (2 * p0 + 1)) |
-                                      ((uint32_t)(qb.x != 0ull) << (2 * p1)) | ((uint32_t)(qb.y != 0ull) << (2 * p1 + 1));
-                if (fast) slot = bucket_resolve(tab, match, full, (3u << (2 * p0)) | (3u << (2 * p1)), tk.key, home, lo + p);
+                // the home slot's pair (16 B) first; only a lane whose home pair is full without its key
+                // loads the next pair: the vector L1 handles a probe lane by lane (random lines), so the
+                // lanes left out of an instruction are what it saves
+                const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
+                ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
+                if (fast) qa = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + start);
+                uint32_t match = (uint32_t)(qa.x == tk.key) | ((uint32_t)(qa.y == tk.key) << 1);
+                uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
+                if (fast && !(match | empty)) {
+                    qb = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + ((start + 2) & (kBucket - 2)));
+                    match |= ((uint32_t)(qb.x == tk.key) << 2) | ((uint32_t)(qb.y == tk.key) << 3);
+                    empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
+                }
+                if (fast) slot = bucket_resolve(tab, match, empty, tk.key, bbase, start, lo + p);
             }
             const bool resolved = fast && slot != kSlotNone;
-            const uint64_t ri = rec_slot(cbase, cap, rot, out + q);
+            const uint64_t ri = rec_slot(cbase, wrap, rot, out + q);
             if (resolved) {
                 const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, lo + p)];
                 rec[ri] = ((uint64_t)slot << 32) | f;
@@ -837,8 +919,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
             const bool pf = fast && !resolved, ps = valid && !fast;
             const uint64_t mf = __ballot(pf), ms = __ballot(ps);
             const uint32_t e = (pbase + p) | ((out + q) << 16);
-            if (pf) pend[cbase + npf + (uint32_t)__popcll(mf & lt)] = e;
-            if (ps) pend[pend_end - 1 - (nps + (uint32_t)__popcll(ms & lt))] = e;
+            if (pf) pend[cbase + npf + lanes_below(mf)] = e;
+            if (ps) pend[pend_end - 1 - (nps + lanes_below(ms))] = e;
             npf += (uint32_t)__popcll(mf);
             nps += (uint32_t)__popcll(ms);
         }
@@ -849,9 +931,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (!(kAblate & 16)) {
-        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, cap, rot, pend_end, pend,
+        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, pend_end, pend,
                                npf, tab, rec, W.hist, longs, long_per);
-        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, cap, rot, pend_end, pend,
+        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, pend_end, pend,
                               nps, tab, rec, W.hist, longs, long_per);
     }
     wave_sync();

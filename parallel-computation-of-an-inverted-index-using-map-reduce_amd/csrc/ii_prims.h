@@ -33,6 +33,10 @@ __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ uint64_t lanemask_lt() {
     return (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
 }
+// set bits of the wave mask m below this lane (v_mbcnt_lo + v_mbcnt_hi)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // Inclusive wave64 scan of a u64 value.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
