@@ -73,7 +73,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 //              whose hot bucket was already full.
 // A word lives in exactly one place: a probe scans the same bucket (then the
 // same big-table run) in the same order and slots only go empty -> full.
-constexpr int kHotLog2 = 20;  // hot level: 2^20 slots (8 MB of keys) in 8-slot buckets (vs 2^19: K1c 5.1 -> 3.4 ms
+constexpr int kHotLog2 = 20;  // hot level: 2^20 slots (8 MB of keys) in 8-slot buckets (2^19: emit 14.6 -> 16.5 ms, 2^18: 18.4 ms
+                              // at 10 GB with K1c fused; earlier, separate K1c: 2^19 -> 2^20: K1c 5.1 -> 3.4 ms
                               // at 10 GB, fewer words overflow to the big table)
 constexpr uint64_t kHotSlots = 1ull << kHotLog2;
 constexpr int kBucket = 8;
