@@ -293,11 +293,13 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             if (wid)
                 k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
                     *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist);
+                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist,
+                    P_<uint32_t>(c->chunk_files));
             else
                 k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
                     *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist);
+                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist,
+                    P_<uint32_t>(c->chunk_files));
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
             if (sweep) k_digit_bases<<<kLaterDigits, kRadix, 0, c->st>>>(dhist, dhist + kLaterDigits * kRadix);
@@ -499,6 +501,15 @@ static bool use_fixed_capacity(ii_ctx* c, uint64_t nch, bool dense) {
     return 12.0 * (double)nch * (double)kChunkCap <= 0.4 * ((double)fr + held);
 }
 
+// Room for fast-path miss keys in a narrow chunk (kNarrowKeys); tests lower it
+// with II_NARROW_KEYS to drive the overflow path on ordinary corpora.
+static uint32_t narrow_keys() {
+    const char* e = getenv("II_NARROW_KEYS");
+    if (!e || !*e) return (uint32_t)kNarrowKeys;
+    const unsigned long v = strtoul(e, nullptr, 10);
+    return v < kNarrowKeys ? (uint32_t)v : (uint32_t)kNarrowKeys;
+}
+
 // dense: records of token k at rec[k] (the import path indexes them so)
 static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = false) {
     c->mapped = c->have_pairs = c->reduced = false;
@@ -575,7 +586,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
                                                        P_<uint32_t>(c->chunk_files), P_<LongTok>(c->longs),
-                                                       c->long_cap / kLongShards);
+                                                       c->long_cap / kLongShards, narrow_keys());
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         k_long_totals<<<1, 64, 0, c->st>>>(counters);
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));

@@ -475,13 +475,24 @@ __device__ __forceinline__ uint32_t chunk_rot(uint64_t c) {
 __device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64_t cap, uint64_t c) {
     return cap ? c * cap : chunk_off[c];
 }
-// index of the chunk's j-th record: cbase from chunk_base, (rot, wrap) =
-// (chunk_rot(c), kChunkCap - 1) in the fixed-capacity layout, (0, ~0) dense
+// Narrow records: in the fixed-capacity layout, a chunk that lies inside one
+// file (k_chunk_files: first file == last file, ~98 % of config3's chunks)
+// stores its records as u32 word slots in the first half of its slot (the
+// file id is the chunk's, restored by the first sort pass), which halves the
+// record bytes K1b writes and the first sort pass reads.  Its fast-path misses
+// keep their keys in the second half (kNarrowKeys u64 entries, in miss order);
+// a chunk with more misses than that (narrow_keys, kNarrowKeys unless a test
+// lowers it with II_NARROW_KEYS) sends the rest down the general path.
+constexpr uint32_t kNarrowKeys = (uint32_t)(kChunkCap / 2);
+__device__ __forceinline__ bool chunk_narrow(uint64_t cap, const uint32_t* cf, uint64_t c) {
+    return cap && cf[3 * c] == cf[3 * c + 1];
+}
+// the chunk's j-th record sits at cbase (chunk_base) + ((j + rot) & wrap), (rot,
+// wrap) = (chunk_rot(c), kChunkCap - 1) in the fixed-capacity layout (u32
+// units for a narrow chunk), (0, ~0) in the dense one
 __device__ __forceinline__ uint32_t rec_wrap(uint64_t cap) { return cap ? (uint32_t)(kChunkCap - 1) : ~0u; }
 __device__ __forceinline__ uint32_t rec_rot(uint64_t cap, uint64_t c) { return cap ? chunk_rot(c) : 0u; }
-__device__ __forceinline__ uint64_t rec_slot(uint64_t cbase, uint32_t wrap, uint32_t rot, uint32_t j) {
-    return cbase + ((j + rot) & wrap);
-}
+
 
 // ---------------------------------------------------------------- K1b emit
 // One wave per chunk (see "K1 chunks"), in rounds of kRound bytes: 2 windows
@@ -758,7 +769,7 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                                                 const uint64_t* __restrict__ file_start,
                                                 const uint32_t* __restrict__ file_id, uint32_t f_lo, uint32_t f_hi,
                                                 uint32_t fid0, uint64_t cbase, uint32_t wrap, uint32_t rot,
-                                                uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
+                                                bool narrow, uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
                                                 const Table& tab, uint64_t* __restrict__ rec, uint32_t* hist,
                                                 LongTok* __restrict__ longs, uint64_t long_per) {
     const int l = lane_id();
@@ -770,7 +781,7 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
         if (i < n) {
             const uint32_t e = kSlow ? pend[pend_end - 1 - i] : pend[cbase + i];
             pos = chunk_lo + (e & 0xFFFFu);
-            const uint64_t r = rec_slot(cbase, wrap, rot, e >> 16);
+            const uint32_t jr = ((e >> 16) + rot) & wrap;  // the token's record in the chunk's slot
             uint64_t key;
             if (kSlow) {
                 const TokKey k = general_key(text, nbytes, pos, tab.seed);
@@ -778,11 +789,15 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                 key = k.key;
                 is_long = k.nlet > 12;
             } else {
-                key = rec[r];
+                key = rec[cbase + (narrow ? kNarrowKeys + i : jr)];
             }
             slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-            const uint32_t f = f_lo == f_hi ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
-            rec[r] = (slot << 32) | f;
+            if (narrow) {
+                reinterpret_cast<uint32_t*>(rec + cbase)[jr] = (uint32_t)slot;
+            } else {
+                const uint32_t f = f_lo == f_hi ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
+                rec[cbase + jr] = (slot << 32) | f;
+            }
         }
         if (!kSlow) continue;
         // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
@@ -815,7 +830,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                      uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
                                                      const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
-                                                     uint64_t long_per) {
+                                                     uint64_t long_per, uint32_t narrow_keys) {
     __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
     const uint64_t c = wave_chunk();
     if (c >= nch) return;
@@ -826,7 +841,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     // the chunk's files (k_chunk_files), wave-uniform
     const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
     const bool fsame = f_lo == f_hi;
+    const bool narrow = chunk_narrow(cap, cf, c);
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
+    uint32_t* const rec32 = reinterpret_cast<uint32_t*>(rec + cbase);
     const uint32_t rot = rec_rot(cap, c), wrap = rec_wrap(cap);
     uint32_t out = 0;               // records emitted so far (wave-uniform)
     uint32_t npf = 0, nps = 0;      // tokens left to K1c: fast-path misses, general-path tokens
@@ -908,17 +925,28 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
                 if (fast) slot = bucket_resolve(tab, match, empty, tk.key, bbase, start, lo + p);
             }
             const bool resolved = fast && slot != kSlotNone;
-            const uint64_t ri = rec_slot(cbase, wrap, rot, out + q);
+            bool pf = fast && !resolved, ps = valid && !fast;
+            uint64_t mf = __ballot(pf);
+            if (narrow && npf + (uint32_t)__popcll(mf) > narrow_keys) {  // (wave-uniform, adversarial) no room for
+                if (!(kAblate & 4) && pf) atomicSub(&W.hist[tk.first], 1u);  // more keys: K1c re-reads them from the
+                ps = ps || pf;                                                // text (and counts their letters)
+                pf = false;
+                mf = 0;
+            }
+            const uint32_t jr = (out + q + rot) & wrap;  // this token's record in the chunk's slot
             if (resolved) {
-                const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, lo + p)];
-                rec[ri] = ((uint64_t)slot << 32) | f;
-            } else if (fast) {
-                rec[ri] = tk.key;
+                if (narrow) {
+                    rec32[jr] = slot;
+                } else {
+                    const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, lo + p)];
+                    rec[cbase + jr] = ((uint64_t)slot << 32) | f;
+                }
+            } else if (pf) {
+                rec[cbase + (narrow ? kNarrowKeys + npf + lanes_below(mf) : jr)] = tk.key;
             }
             // pending: fast-path misses from the front of the chunk's list, general-path tokens
             // from its back, so that K1c runs each kind without divergence
-            const bool pf = fast && !resolved, ps = valid && !fast;
-            const uint64_t mf = __ballot(pf), ms = __ballot(ps);
+            const uint64_t ms = __ballot(ps);
             const uint32_t e = (pbase + p) | ((out + q) << 16);
             if (pf) pend[cbase + npf + lanes_below(mf)] = e;
             if (ps) pend[pend_end - 1 - (nps + lanes_below(ms))] = e;
@@ -932,9 +960,9 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (!(kAblate & 16)) {
-        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, pend_end, pend,
+        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, narrow, pend_end, pend,
                                npf, tab, rec, W.hist, longs, long_per);
-        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, pend_end, pend,
+        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, narrow, pend_end, pend,
                               nps, tab, rec, W.hist, longs, long_per);
     }
     wave_sync();
@@ -1301,10 +1329,12 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                                                            uint32_t nchunks, uint64_t* __restrict__ table,
                                                            const uint32_t* __restrict__ remap,
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
-                                                           int shift1, int shift2, uint64_t* __restrict__ dhist) {
+                                                           int shift1, int shift2, uint64_t* __restrict__ dhist,
+                                                           const uint32_t* __restrict__ cf) {
     __shared__ uint32_t cnt[kCWaves][kRadix];
     __shared__ uint32_t bm[kDedupWords];
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
+    __shared__ uint32_t s_cfid[kCMaxGroup];      // narrow chunk: its file id; ~0: u64 records
     __shared__ uint32_t s_later[kLaterDigits][kRadix];
     __shared__ uint32_t s_wtot[2][kCWaves];      // per tile parity: one barrier per tile
     __shared__ uint32_t s_last[2];               // per tile parity: file of the tile's last record
@@ -1315,6 +1345,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
     for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
+    for (uint32_t i = threadIdx.x; i < ng; i += kCBlock) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
     __syncthreads();
     const uint64_t tofs = (uint64_t)w * 64 * kS0Items + l;
     const uint64_t lt = lanemask_lt();
@@ -1324,16 +1355,24 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint32_t gnext = s_voff[1];                      // first WG-relative index past chunk g
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
+    uint32_t gfid = ng ? s_cfid[0] : ~0u;            // narrow chunk's file (~0: u64 records)
     uint64_t o = lo;  // next output position
     // The next tile's records are loaded while this one is written: issued
     // after this tile's remap gathers have been consumed (vmcnt is in order, so
     // a prefetch issued before them would make the gathers wait for it).
+    // A narrow chunk's record is the u32 half (nodd bit) of the u64 loaded, its
+    // file the chunk's (nfid); one load form for both kinds, so the loads stay
+    // in flight (a branch between two load forms would wait for them).
     uint64_t nraw[kS0Items];
+    uint32_t nfid[kS0Items];  // narrow item: its chunk's file id; ~0: a u64 record
+    uint32_t nodd = 0;
     auto load_tile = [&](uint64_t tb) {
+        nodd = 0;
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             const uint64_t idx = tb + tofs + (uint64_t)k * 64;
             uint64_t src = idx;
+            nfid[k] = ~0u;
             if (cap && idx < hi) {
                 const uint32_t ri = (uint32_t)(idx - lo);
                 if (ri >= gnext) {
@@ -1344,20 +1383,26 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                     } while (ri >= gnext);
                     gadj = chunk_rot(c0 + g) - gs;
                     gbase = (uint64_t)(c0 + g) * cap;
+                    gfid = s_cfid[g];
                 }
-                src = gbase + ((ri + gadj) & (uint32_t)(kChunkCap - 1));
+                const uint32_t j = (ri + gadj) & (uint32_t)(kChunkCap - 1);
+                nfid[k] = gfid;
+                const bool nw = gfid != ~0u;
+                nodd |= (uint32_t)(nw && (j & 1u)) << k;
+                src = gbase + (nw ? j >> 1 : j);
             }
             nraw[k] = idx < hi ? ld_nt(keys + src) : 0ull;
         }
     };
     if (lo < hi) load_tile(lo);
     // the first tile's epoch: the file of the range's first record (every lane loads it)
-    uint32_t epoch = lo < hi ? (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo] : 0u;
+    uint32_t epoch = lo >= hi ? 0u : s_cfid[0] != ~0u ? s_cfid[0] : (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo];
     uint32_t par = 0;
     for (uint64_t tb = lo; tb < hi; tb += kCTile, par ^= 1u) {
         uint64_t raw[kS0Items];
 #pragma unroll
-        for (int k = 0; k < kS0Items; k++) raw[k] = nraw[k];
+        for (int k = 0; k < kS0Items; k++)
+            raw[k] = nfid[k] == ~0u ? nraw[k] : ((nraw[k] >> (32 * ((nodd >> k) & 1u))) << 32) | nfid[k];
         if (tb != lo && s_last[par ^ 1u] != epoch) {  // (workgroup-uniform) a new file: clear the bitmap
             epoch = s_last[par ^ 1u];
             for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;

@@ -64,7 +64,7 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
         k_tok_emit<A><<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, tab, rec, chist, pend, pcnt, cf,
-                                      longs, lcap / kLongShards);
+                                      longs, lcap / kLongShards, (uint32_t)kNarrowKeys);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));

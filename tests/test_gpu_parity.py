@@ -250,6 +250,28 @@ def test_record_layouts_vs_oracle():
     assert counts["dense"] == counts["fixed"]
 
 
+def test_narrow_key_overflow_vs_oracle():
+    """Narrow (u32) records: a single-file chunk keeps its fast-path misses'
+    keys in a bounded area; II_NARROW_KEYS lowers that bound so that the
+    overflow path (the rest go down K1c's general path, letter counts
+    corrected) runs on an ordinary corpus whose vocabulary overflows the hot
+    table (many misses per chunk)."""
+    t, off = ii_ctypes.zipf_corpus(24_000_000, 40, 3_000_000, 29, threads=8)
+    ids = list(range(40))
+    exp = oracle_index(t, off, ids)
+    for cap in ["0", "5", "64"]:
+        os.environ["II_NARROW_KEYS"] = cap
+        try:
+            ix = ii_ctypes.Index(0)
+            ix.map_host(t, off.tolist(), ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, "narrow keys " + cap)
+            assert ix.stats().resolved_tokens > 0
+            ix.close()
+        finally:
+            del os.environ["II_NARROW_KEYS"]
+
+
 # ---------------------------------------------------------------- multi-GPU exchange logic
 def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False):
     """G logical shards on one device: files split by the reference's size
