@@ -59,6 +59,7 @@ struct ii_ctx {
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
     DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
+    DBuf uniq_x, pstart_x;  // exchange after a word-id reduce: the pairs in lexid order (letter_points)
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
@@ -66,6 +67,7 @@ struct ii_ctx {
     uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
     uint64_t lb_epoch = 0;       // epoch of the last onesweep pass
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
+    bool xpairs = false;    // uniq_x / pstart_x hold this partial index's pairs in lexid order
     uint64_t NW = 0;        // wid range
     // partial-file emitter (ii_partials)
     DBuf ppieces, pcnt, pout, ploff;
@@ -365,6 +367,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
 // (post_start[V] = U).  Sets c->U.
 static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false) {
+    c->xpairs = false;
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
     CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
@@ -447,7 +450,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
-                   &c->dhist,    &c->lbstat, &c->ticket};
+                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -1119,7 +1122,7 @@ extern "C" int ii_reduce_local(ii_ctx* c) {
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
     if (c->have_pairs) return II_OK;
-    return local_reduce(c);
+    return local_reduce(c, true);
 }
 
 extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
@@ -1132,18 +1135,35 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
 
 // ----------------------------------------------------------------- exchange
 // Per-letter points of the partial index (first word / pair / arena byte).
+// After a word-id reduce the exported pairs come from a lexid-ordered copy
+// (uniq_x / pstart_x, k_pairs_by_lexid), made once per reduce.
+static const uint64_t* export_pairs(ii_ctx* c) { return P_<uint64_t>(c->wid_pairs ? c->uniq_x : c->uniq); }
 static int letter_points(ii_ctx* c) {
     const uint64_t V = c->V;
-    if (c->wid_pairs) return II_ERR_STATE;  // after ii_reduce: the exchange needs ii_reduce_local first
     if (V == 0 || c->T == 0) {
         memset(c->h_pts, 0, sizeof(c->h_pts));
         return II_OK;
+    }
+    const uint64_t* ps = P_<uint64_t>(c->pstart);
+    if (c->wid_pairs) {
+        CK(grow(c->pstart_x, sizeof(uint64_t) * (V + 1)));
+        CK(grow(c->uniq_x, sizeof(uint64_t) * std::max<uint64_t>(c->U, 1)));
+        uint64_t* psx = P_<uint64_t>(c->pstart_x);
+        if (!c->xpairs) {
+            CK(run_scan(c, OpRunLen{ps, P_<uint64_t>(c->pstop), psx}, V, psx + V));
+            if (c->U)
+                k_pairs_by_lexid<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(
+                    P_<uint64_t>(c->uniq), c->U, P_<uint32_t>(c->lexw), ps, psx, P_<uint64_t>(c->uniq_x));
+            HIPCK(hipGetLastError());
+            c->xpairs = true;
+        }
+        ps = psx;
     }
     CK(grow(c->woff, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->pts, sizeof(uint64_t) * 3 * (II_ALPHABET + 1)));
     uint64_t* woff = P_<uint64_t>(c->woff);
     CK(run_scan(c, OpWordArena{P_<uint32_t>(c->llen), woff}, V, woff + V));
-    k_letter_points<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), P_<uint64_t>(c->pstart), woff, P_<uint64_t>(c->pts));
+    k_letter_points<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), ps, woff, P_<uint64_t>(c->pts));
     HIPCK(hipGetLastError());
     CK(read_u64(c, c->pts.p, c->h_pts, 3 * (II_ALPHABET + 1)));
     return II_OK;
@@ -1172,7 +1192,7 @@ static int plan_core(ii_ctx* c, int nparts, const int* lo_in, const int* hi_in, 
     }
     if (c->part_hi[nparts - 1] != II_ALPHABET) return II_ERR_ARG;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c));
+    if (!c->have_pairs) CK(local_reduce(c, true));
     CK(letter_points(c));
     for (int r = 0; r < nparts; r++) {
         const uint64_t* a = c->h_pts + 3 * c->part_lo[r];
@@ -1197,7 +1217,7 @@ extern "C" int ii_letter_load(ii_ctx* c, uint64_t pairs[II_ALPHABET]) {
     if (!c || !pairs) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c));
+    if (!c->have_pairs) CK(local_reduce(c, true));
     CK(letter_points(c));
     for (int l = 0; l < II_ALPHABET; l++) pairs[l] = c->h_pts[3 * (l + 1) + 1] - c->h_pts[3 * l + 1];
     return II_OK;
@@ -1221,7 +1241,7 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
         k_export_header<<<1, 64, 0, c->st>>>((uint64_t*)seg, nw, np, ab, lo, hi, id_lo1, id_hi1);
         if (np)
             k_export_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
-                P_<uint64_t>(c->uniq), a[1], b[1], (uint32_t)a[0], pairs);
+                export_pairs(c), a[1], b[1], (uint32_t)a[0], pairs);
         if (nw)
             k_export_words<<<grid_for(nw), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey),
                                                               P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen),

@@ -1870,6 +1870,30 @@ struct OpWordArena {
     __device__ void emit(uint64_t j, uint64_t ex, uint64_t) const { woff[j] = ex; }
 };
 
+// Exchange after a word-id reduce: the pairs re-laid out in lexicographic
+// word order (the order export segments carry), keyed by lexid: pair s
+// (grouped by word id) of word j = lexw[wid] goes to psx[j] + (s - ps[j]),
+// psx = exclusive scan of the words' pair counts in lexid order.  One read
+// and one write per pair instead of sorting the tokens by lexid (whose first
+// pass gathers a map entry for every word).
+struct OpRunLen {
+    const uint64_t* ps;
+    const uint64_t* pe;
+    uint64_t* psx;
+    __device__ uint64_t value(uint64_t j) const { return pe[j] - ps[j]; }
+    __device__ void emit(uint64_t j, uint64_t ex, uint64_t) const { psx[j] = ex; }
+};
+__global__ __launch_bounds__(kBlock) void k_pairs_by_lexid(const uint64_t* __restrict__ uniq, uint64_t U,
+                                                           const uint32_t* __restrict__ lexw,
+                                                           const uint64_t* __restrict__ ps,
+                                                           const uint64_t* __restrict__ psx, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < U; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t r = uniq[i];
+        const uint32_t j = lexw[r >> 32];
+        out[psx[j] + (i - ps[j])] = ((uint64_t)j << 32) | (r & 0xFFFFFFFFull);
+    }
+}
+
 // per letter l: first word, first pair, first arena byte
 __global__ void k_letter_points(const uint32_t* __restrict__ letter_start, const uint64_t* __restrict__ post_start,
                                 const uint64_t* __restrict__ woff, uint64_t* __restrict__ pts) {
