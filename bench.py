@@ -433,15 +433,16 @@ def main():
         # sort + segmented-reduce phase (K2 token sort + K3 unique), two byte models:
         #  survey: SURVEY §8d — first pass 8T + 8T_k, each radix pass 16 T_k, the unique
         #          pass 8 T_k + 8 U + 16 V (what the algorithm must move)
-        #  impl:   what the kernels of this build move — the later digits are counted
-        #          in the first pass (no histogram reads), the onesweep passes read and
-        #          write each record once, K3 reads them once (one pass, staged in LDS)
-        #          and writes the pairs, the posting offsets P (every word start and
-        #          every 64th pair) and the per-word start / end arrays
+        #  impl:   what the kernels of this build move — the passes after the first
+        #          as the library counts them (st.sort_bytes: the packed form's u32
+        #          bucket passes move 36 B per kept record against 48 for three u64
+        #          passes), K3 reads the records once (one pass, staged in LDS) and
+        #          writes the pairs, the posting offsets P (every word start and every
+        #          64th pair) and the per-word start / end arrays
         T, Tk, U, V = st.tokens, st.sorted_records, st.pairs, st.words
         sp = max(1, st.sort_passes)
         survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
-        impl_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 8 * (V + U // 64) + 16 * V
+        impl_b = 8 * T + 8 * Tk + st.sort_bytes + 8 * Tk + 8 * U + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_gbs = survey_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         cpu = None

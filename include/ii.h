@@ -92,6 +92,10 @@ typedef struct {
      * the bytes uploaded */
     double io_ms;
     uint64_t io_bytes;
+    /* bytes the token sort's passes after the first move (reads + writes of
+     * every scatter / onesweep launch and the packed form's bucket histogram) */
+    uint64_t sort_bytes;
+    uint32_t sort_packed;  /* 1: the packed form (u32 records in buckets, ii_prims.h) ran */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

@@ -64,6 +64,7 @@ struct ii_ctx {
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
+    DBuf msd;                    // packed token sort: bucket geometry, per-bucket digit counts and bases
     uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
     uint64_t lb_epoch = 0;       // epoch of the last onesweep pass
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
@@ -100,6 +101,8 @@ struct ii_ctx {
     uint64_t T_sorted = 0;  // records left after the pass-0 dedup
     hipEvent_t ev_c0[2] = {};  // around k_sort0_compact
     uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
+    bool sort_packed = false;  // the last token sort ran in the packed form (run_sort_packed)
+    uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
     uint64_t n_pending = 0; // tokens K1b left to K1c
     uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
     uint64_t nch_map = 0;   // K1b chunks of the last map
@@ -159,6 +162,8 @@ static inline double now_ms() {
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
+// bytes the packed token sort's u32 layout of n records may take (every bucket padded to whole tiles)
+static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)kRadix * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
 static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
@@ -330,10 +335,12 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
         if (kv)
             k_radix_scatter<true><<<(uint32_t)nch, kBlock, 0, c->st>>>(src, dst, *v, *v2, n, chunk, shift, db,
-                                                                      (uint32_t)nch, table, nullptr);
+                                                                      (uint32_t)nch, table, nullptr, nullptr, nullptr,
+                                                                      0, 0u);
         else
             k_radix_scatter<false, kScatterThreads, kScatterItems><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-                src, dst, nullptr, nullptr, n, chunk, shift, db, (uint32_t)nch, table, first0 ? kept : nullptr);
+                src, dst, nullptr, nullptr, n, chunk, shift, db, (uint32_t)nch, table, first0 ? kept : nullptr, nullptr,
+                nullptr, 0, 0u);
         if (ev) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
             c->n_sc++;
@@ -359,6 +366,114 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             if (kv) std::swap(*v, *v2);
             if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n + (kv ? 8 * n : 0);
         }
+    }
+    return II_OK;
+}
+
+// Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
+// W-bit key when the other W - m key bits and the F id bits fit a u32 and
+// leave two LSD passes of <= kRadixBits bits; 0 = not packable.
+static int packed_top_bits(int W, int F) {
+    if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return 0;
+    const int m = std::max(7, W + F - 32);
+    const int L = W - m;
+    return (m <= kRadixBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
+}
+
+// The token sort of local_reduce in the packed form: k_sort0_compact (dedup,
+// key remap, compaction, counts of the top digit per workgroup) into *k2, the
+// MSD scatter into buckets of u32 records (*k, padded), per-bucket digit
+// counts, two bucket-local onesweep passes (*k -> *k2 -> *k, the last one
+// writing the dense u64 records).  Keys sit at bits [lo, lo + W) of the
+// records, ids below 2^F.  On return *k holds the *n_out sorted records.
+static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F, int m,
+                           const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
+    *passes = 0;
+    *n_out = n;
+    const uint32_t nb = 1u << m;
+    const int L = W - m, b0 = L - L / 2, b1 = L / 2;
+    const uint64_t nch_in = c->nch_map;
+    const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
+    if (nch_in == 0 || group > kCMaxGroup) return II_ERR_NOMEM;
+    const uint64_t nch = (nch_in + group - 1) / group;
+    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
+    CK(grow(c->kept, sizeof(uint64_t) * 2 * kMaxChunks));
+    // msd: bstart[kRadix + 1] | pad[kRadix] | btile (u32)[kRadix + 1] | gh[2 kRadix^2] | gbase[2 kRadix^2]
+    constexpr size_t kGeo = 3 * kRadix + 2;
+    CK(grow(c->msd, sizeof(uint64_t) * (kGeo + 4 * kRadix * kRadix)));
+    uint64_t* bstart = P_<uint64_t>(c->msd);
+    uint64_t* pad = bstart + kRadix + 1;
+    uint32_t* btile = reinterpret_cast<uint32_t*>(pad + kRadix);
+    uint64_t* gh = bstart + kGeo;
+    uint64_t* gbase = gh + 2 * kRadix * kRadix;
+    uint64_t* table = P_<uint64_t>(c->rtable);
+    uint64_t* kept = P_<uint64_t>(c->kept);
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    unsigned long long* err = P_<unsigned long long>(c->counters) + C_OVERFLOW;
+    const int shift = lo + L;  // the top digit of the key
+    const uint32_t dmask = nb - 1u;
+
+    HIPCK(hipEventRecord(c->ev_c0[0], c->st));
+    if (wid)
+        k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
+            *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
+            table, remap0, *k2, kept, 0, 0, nullptr, P_<uint32_t>(c->chunk_files));
+    else
+        k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
+            *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
+            table, remap0, *k2, kept, 0, 0, nullptr, P_<uint32_t>(c->chunk_files));
+    HIPCK(hipEventRecord(c->ev_c0[1], c->st));
+    CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
+    k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);
+    HIPCK(hipMemsetAsync(gh, 0, sizeof(uint64_t) * 2 * nb * kRadix, c->st));
+    HIPCK(hipGetLastError());
+    // MSD scatter: u64 records -> u32 records in padded buckets
+    const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
+    if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
+    k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
+        *k2, nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
+        F, (1u << L) - 1u);
+    if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
+    HIPCK(hipGetLastError());
+    uint64_t t47[4];
+    CK(read_u64(c, totals + 4, t47, 4));
+    const uint64_t n_in = n;
+    n = t47[0];
+    if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
+    c->c0_bytes = 8 * n_in + 8 * n;
+    *n_out = n;
+    if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
+    *passes = 1;
+    if (n == 0) return II_OK;
+    // per-bucket digit counts of the two LSD passes -> bases
+    c->sort_packed = true;
+    c->sort_hist_bytes = 4 * n;
+    const uint64_t ntb = (n + kSweepTile - 1) / kSweepTile + nb;  // tiles of the padded layout, at most
+    const uint32_t hg = (uint32_t)std::min<uint64_t>(kMaxChunks, ntb);
+    const uint32_t per = (uint32_t)((ntb + hg - 1) / hg);
+    k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
+        reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
+    k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
+    HIPCK(hipGetLastError());
+    // two bucket-local onesweep passes: u32 -> u32 (padded), u32 -> u64 (dense)
+    for (int p = 0; p < 2; p++) {
+        CK(lookback_pass(c, ntb * kRadix));
+        const bool evp = c->n_sc < kMaxTimedPasses;
+        if (evp) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
+        if (p == 0)
+            k_onesweep_seg<kSweepThreads, kSweepItems, false><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+                reinterpret_cast<const uint32_t*>(*k), reinterpret_cast<uint32_t*>(*k2), nullptr, btile, bstart, nb, F,
+                b0, gbase, 2 * kRadix, F, L, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err);
+        else
+            k_onesweep_seg<kSweepThreads, kSweepItems, true><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+                reinterpret_cast<const uint32_t*>(*k2), nullptr, *k, btile, bstart, nb, F + b0, b1, gbase + kRadix,
+                2 * kRadix, F, L, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err);
+        if (evp) {
+            HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
+            c->sc_bytes[c->n_sc++] = p == 0 ? 8 * n : 12 * n;
+        }
+        HIPCK(hipGetLastError());
+        (*passes)++;
     }
     return II_OK;
 }
@@ -552,7 +667,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     if (c->rec_cap) {
         CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
         if (hv[1] & 4) return II_ERR_LAYOUT;
-        CK(grow(c->rec, sizeof(uint64_t) * nch * kChunkCap));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, packed_bytes(nch * kChunkCap))));
         CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
         c->T = 0;
     } else {
@@ -562,8 +677,8 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
         if (hv[1] & 4) return II_ERR_LAYOUT;
         c->T = hv[0];
-        CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
-        CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
+        CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
         CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
     }
     CK(grow(c->pend_cnt, sizeof(uint32_t) * nch));
@@ -629,7 +744,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     if (c->rec_cap) {  // chunk token counts -> voff (exclusive scan, voff[nch] = T)
         CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
         CK(read_u64(c, totals, &c->T));
-        CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>(c->T, 1)));
+        CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
     }
     HIPCK(hipMemsetAsync(counters + C_HIST, 0, sizeof(uint64_t) * II_ALPHABET, c->st));
     k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
@@ -1033,8 +1148,15 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     uint64_t* r2 = P_<uint64_t>(c->rec2);
     const int lb = std::max(1, bitlen((wid ? c->NW : V) - 1));
     uint64_t Tk = T;
-    CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
-                P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid));
+    const int F = std::max(1, bitlen(c->id_bound ? c->id_bound - 1 : 0));
+    c->sort_packed = false;
+    const int m = packed_top_bits(lb, F);
+    if (m)
+        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
+                           &sort_passes));
+    else
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
+                    P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid));
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
@@ -1487,7 +1609,9 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         }
         s.scatter_launches = (uint32_t)c->n_sc;
         s.scatter_ms_avg = c->n_sc ? sum / c->n_sc : 0;
-        s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: 8 B read per record in, 8 B written per record out
+        s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: bytes read + written
+        s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
+        s.sort_packed = c->sort_packed ? 1u : 0u;
         s.sorted_records = c->T_sorted;
         if (c->c0_bytes) {
             s.sort0_ms = ev_ms(c->ev_c0[0], c->ev_c0[1]);

@@ -278,35 +278,36 @@ __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, uint64
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
-// the four bit-7 flags -> a 4-bit mask
-__device__ __forceinline__ uint32_t hb4(uint32_t m) {
-    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
-}
 struct Classes {
     uint32_t ws, letter, nul;  // 16-bit masks over the lane's window
 };
-__device__ __forceinline__ void classify4(uint32_t x, uint32_t& ws, uint32_t& let, uint32_t& nul) {
+// class flags of 4 bytes: bit 7 of each byte (nothing else) set where the byte is of the class
+__device__ __forceinline__ void classify_flags4(uint32_t x, uint32_t& ws, uint32_t& let, uint32_t& nul) {
     const uint32_t hb = x & 0x80808080u;
     const uint32_t y = x & 0x7F7F7F7Fu;
     const uint32_t sp = zero_bytes(x ^ 0x20202020u);                                  // ' '
     const uint32_t ctl = (y + 0x77777777u) & ~(y + 0x72727272u) & ~hb & 0x80808080u;   // 9..13
-    ws = hb4(sp | ctl);                                   // C-locale isspace (main.c:102)
+    ws = sp | ctl;                                        // C-locale isspace (main.c:102)
     const uint32_t z = (x | 0x20202020u) & 0x7F7F7F7Fu;
-    let = hb4((z + 0x1F1F1F1Fu) & ~(z + 0x05050505u) & ~hb & 0x80808080u);  // A-Z / a-z (main.c:106-110)
-    nul = hb4(zero_bytes(x));
+    let = (z + 0x1F1F1F1Fu) & ~(z + 0x05050505u) & ~hb & 0x80808080u;  // A-Z / a-z (main.c:106-110)
+    nul = zero_bytes(x);
+}
+// The bit-7 flags of 16 bytes (f0 = bytes 0..3, ...) -> a 16-bit mask: each
+// flag byte (0x80 or 0) times its bit's weight, summed by v_dot4_u32_u8 (two
+// per 8 bits, weights 1..128 / 128 each) instead of shifting every flag into place.
+__device__ __forceinline__ uint32_t flags16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3) {
+    const uint32_t lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
+    return (lo >> 7) | ((hi >> 7) << 8);
 }
 __device__ __forceinline__ Classes classify16(const uint4& v) {
-    Classes c{0, 0, 0};
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint32_t a, b, n;
-        classify4(w[k], a, b, n);
-        c.ws |= a << (4 * k);
-        c.letter |= b << (4 * k);
-        c.nul |= n << (4 * k);
-    }
-    return c;
+    uint32_t ws[4], let[4], nul[4];
+    classify_flags4(v.x, ws[0], let[0], nul[0]);
+    classify_flags4(v.y, ws[1], let[1], nul[1]);
+    classify_flags4(v.z, ws[2], let[2], nul[2]);
+    classify_flags4(v.w, ws[3], let[3], nul[3]);
+    return Classes{flags16(ws[0], ws[1], ws[2], ws[3]), flags16(let[0], let[1], let[2], let[3]),
+                   flags16(nul[0], nul[1], nul[2], nul[3])};
 }
 
 // Kept tokens among the starts (a letter before the first whitespace / NUL,
@@ -1000,24 +1001,42 @@ struct OpOccupied {
     __device__ void emit(uint64_t, uint64_t, uint64_t) const {}
 };
 
-// Next letter (0..25) of a cleaned word at *g, or 26 once the word has ended
-// (whitespace, NUL, end of text, or 299 letters).
-__device__ __forceinline__ uint32_t next_letter(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t* g,
-                                                uint32_t* n) {
-    if (*n >= (uint32_t)kMaxWord) return 26u;
-    while (*g < nbytes) {
-        uint32_t c = text[*g];
-        if (c == 0u || is_ws(c)) break;
-        (*g)++;
-        uint32_t lc = letter_of(c);
-        if (lc < 26u) {
-            (*n)++;
-            return lc;
+// Letter walk of a cleaned word (main.c:105-111) over cached aligned 16-byte
+// blocks: one load per block instead of a dependent byte load per letter; the
+// block's letter / terminator masks find the next letter without a byte loop.
+struct LetterCursor {
+    uint64_t g;      // next byte to look at
+    uint64_t base;   // cached block (~0: none)
+    uint32_t let, term;
+    uint4 blk;
+    uint32_t n;      // letters returned
+    // next letter (0..25), or 26 once the word has ended (whitespace, NUL, end
+    // of text — load16 reads it as spaces — or 299 letters)
+    __device__ __forceinline__ uint32_t next(const uint8_t* __restrict__ text, uint64_t nbytes) {
+        if (n >= (uint32_t)kMaxWord) return 26u;
+        for (;;) {
+            const uint64_t b = g & ~15ull;
+            if (b != base) {
+                base = b;
+                blk = load16(text, nbytes, (int64_t)b);
+                const Classes cl = classify16(blk);
+                let = cl.letter;
+                term = cl.ws | cl.nul;
+            }
+            const uint32_t j = (uint32_t)(g & 15u);
+            const uint32_t ev = ((let | term) >> j) & 0xFFFFu;
+            if (!ev) {
+                g = b + 16;
+                continue;
+            }
+            const uint32_t i = j + __builtin_ctz(ev);
+            if ((term >> i) & 1u) return 26u;  // ended: g stays at the terminator
+            g = b + i + 1;
+            n++;
+            return letter_of(byte_dyn(blk, i));
         }
     }
-    *g = nbytes;
-    return 26u;
-}
+};
 
 // byte mask (0xFF per selected byte) of the low 4 bits of m, one bit per byte
 __device__ __forceinline__ uint32_t byte_mask4(uint32_t m) { return ((m & 0xFu) * 0x00204081u & 0x01010101u) * 0xFFu; }
@@ -1059,10 +1078,10 @@ __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restric
         LongTok lt = q[i];
         uint64_t a = lt.pos, b = rep[lt.slot];
         if (a == b || same_raw_token(text, nbytes, a, b)) continue;
-        uint32_t na = 0, nb = 0;
+        LetterCursor ca{a, ~0ull, 0u, 0u, make_uint4(0, 0, 0, 0), 0u}, cb{b, ~0ull, 0u, 0u, make_uint4(0, 0, 0, 0), 0u};
         for (;;) {
-            uint32_t la = next_letter(text, nbytes, &a, &na);
-            uint32_t lb = next_letter(text, nbytes, &b, &nb);
+            const uint32_t la = ca.next(text, nbytes);
+            const uint32_t lb = cb.next(text, nbytes);
             if (la != lb) {
                 atomicOr((unsigned long long*)&counters[C_COLLIDE], 1ull);
                 break;
@@ -1829,20 +1848,36 @@ __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict
             // last posting of the word: the next pair belongs to another word (runs are contiguous)
             const bool last = p + 1 == U || wn[k] != w;
             const uint64_t o = fb[k] + pb[k] + (inc - len);
-            if (id <= 0xFFFFFFFFull) {
+            if (nd <= 7u) {
+                // digits + separator (<= 8 bytes) built in one register (each lower digit pushes
+                // the bytes after it up one place), then stored with at most three sized stores
+                // (unaligned global stores are native on gfx950): one byte store per digit made
+                // the pass issue-bound
+                uint64_t s = (uint64_t)(last ? ']' : ' ');
                 uint32_t v = (uint32_t)id;
-                for (int i = (int)nd - 1; i >= 0; i--) {
-                    out[o + i] = (uint8_t)('0' + v % 10u);
+                for (uint32_t i = 0; i < nd; i++) {
+                    s = (s << 8) | (uint64_t)('0' + v % 10u);
                     v /= 10u;
                 }
-            } else {  // id0 = 2^32 - 1
+                uint8_t* d = out + o;
+                if (len == 8u) {
+                    __builtin_memcpy(d, &s, 8);
+                } else {
+                    const uint32_t lo4 = (uint32_t)s;
+                    if (len & 4u) __builtin_memcpy(d, &lo4, 4);
+                    const uint64_t t = s >> (8 * (len & 4u));
+                    const uint16_t t2 = (uint16_t)t;
+                    if (len & 2u) __builtin_memcpy(d + (len & 4u), &t2, 2);
+                    if (len & 1u) d[len & 6u] = (uint8_t)(t >> (8 * (len & 2u)));
+                }
+            } else {  // ids >= 10^7: one byte per digit
                 uint64_t v = id;
                 for (int i = (int)nd - 1; i >= 0; i--) {
                     out[o + i] = (uint8_t)('0' + v % 10u);
                     v /= 10u;
                 }
+                out[o + nd] = last ? ']' : ' ';
             }
-            out[o + nd] = last ? ']' : ' ';
         }
     }
 }

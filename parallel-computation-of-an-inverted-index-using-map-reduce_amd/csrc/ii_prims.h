@@ -224,12 +224,17 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 // NT = 512 every digit's output run is twice as long as with 256 (the store
 // side is what bounds the pass: 6-bit passes, with twice the run length of
 // 7-bit ones, run ~15 % faster).  Threads t < kRadix own one digit each.
-template <bool kHasVals, int NT = kBlock, int IT = kSortItems>
+// kPack (the MSD pass of the packed token sort, see k_onesweep_seg): the
+// record (key << 32 | id) goes out as the u32 (key & pack_low) << pack_f | id
+// — the digit (the key's top bits) is implied by the bucket it lands in — and
+// digit d's output starts pad[d] records later (buckets padded to whole tiles).
+template <bool kHasVals, int NT = kBlock, int IT = kSortItems, bool kPack = false>
 __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                       const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
                                                       uint64_t n, uint64_t chunk, int shift, int dbits,
                                                       uint32_t nchunks, const uint64_t* __restrict__ table,
-                                                      const uint64_t* __restrict__ kept) {
+                                                      const uint64_t* __restrict__ kept, uint32_t* __restrict__ kout32,
+                                                      const uint64_t* __restrict__ pad, int pack_f, uint32_t pack_low) {
     constexpr int NW = NT / 64;
     constexpr int kTileN = NT * IT;
     constexpr int kDW = kRadix / 64;  // waves that own digits
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
     const uint32_t dmask = (1u << dbits) - 1u;
     const uint64_t lo = kept ? kept[kMaxChunks + blockIdx.x] : (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = kept ? lo + kept[blockIdx.x] : (lo + chunk < n ? lo + chunk : n);
-    if (digit_thread) s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x];
+    if (digit_thread) s_run[t] = table[(uint64_t)t * nchunks + blockIdx.x] + (kPack ? pad[t] : 0ull);
     const uint64_t lt = lanemask_lt();
 
     // the next tile's keys are loaded while this tile is ranked and written
@@ -352,7 +357,8 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
                 const uint64_t k = s_keys[p];
                 const uint32_t d = (uint32_t)(k >> shift) & dmask;
                 const uint64_t dst = s_run[d] + (p - s_tstart[d]);
-                kout[dst] = k;
+                if (kPack) kout32[dst] = (((uint32_t)(k >> 32) & pack_low) << pack_f) | (uint32_t)k;
+                else kout[dst] = k;
                 if (kHasVals) vout[dst] = s_vals[p];
             }
         }
@@ -564,6 +570,309 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
             const uint64_t k = s_keys[p];
             const uint32_t d = (uint32_t)(k >> shift) & dmask;
             kout[s_run[d] + (p - s_tstart[d])] = k;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Packed token sort (MSD bucket, then LSD inside the buckets, u32 records).
+// The token records are key << 32 | id with a key of W bits and ids of F bits;
+// when W - m + F <= 32 for an m-bit top digit, the first scatter partitions
+// the records by the key's top m bits (k_radix_scatter<kPack>) into buckets
+// padded to whole onesweep tiles and writes each as the u32
+// low << F | id (low = the key's other W - m bits): the bucket implies the top
+// digit.  The remaining digits are sorted inside each bucket by onesweep passes
+// over the u32 records (k_onesweep_seg): a tile lies in one bucket and looks
+// back only over its bucket's tiles.  The last pass writes the full u64
+// records at their dense places.  Against three u64 passes this moves 36
+// instead of 48 bytes per record (8 + 4 scatter, 4 histogram, 4 + 4, 4 + 8).
+//
+// Bucket geometry (one workgroup): bstart[h] = dense start of bucket h (the
+// exclusive scan of the MSD scatter's digit-major table, column 0) and
+// bstart[nb] = the total; btile[h] = its first tile in the padded layout
+// (btile[nb] = all tiles); pad[h] = btile[h] * tile - bstart[h].
+__global__ __launch_bounds__(kRadix) void k_msd_geometry(const uint64_t* __restrict__ table, uint32_t nchunks,
+                                                         uint32_t nb, const uint64_t* __restrict__ total, uint32_t tile,
+                                                         uint64_t* __restrict__ bstart, uint32_t* __restrict__ btile,
+                                                         uint64_t* __restrict__ pad) {
+    __shared__ uint64_t lds[kRadix / 64 + 1];
+    const uint32_t h = threadIdx.x;
+    const uint64_t tot = *total;
+    const uint64_t s = h < nb ? table[(uint64_t)h * nchunks] : tot;
+    const uint64_t e = h + 1 < nb ? table[(uint64_t)(h + 1) * nchunks] : tot;
+    const uint64_t nt = h < nb ? (e - s + tile - 1) / tile : 0;
+    const uint64_t inc = wave_incl_scan(nt);
+    if (lane_id() == 63) lds[wave_id()] = inc;
+    __syncthreads();
+    uint64_t base = 0, all = 0;
+    for (int w = 0; w < kRadix / 64; w++) {
+        if (w < wave_id()) base += lds[w];
+        all += lds[w];
+    }
+    const uint64_t t0 = base + inc - nt;
+    if (h < nb) {
+        bstart[h] = s;
+        btile[h] = (uint32_t)t0;
+        pad[h] = t0 * tile - s;
+    }
+    if (h == 0) {
+        bstart[nb] = tot;
+        btile[nb] = (uint32_t)all;
+    }
+}
+
+// Per-bucket counts of the two LSD digits of the packed records:
+// gh[(2 h + j) * kRadix + d] += records of bucket h whose digit j is d (digit j
+// = bits [s_j, s_j + b_j) of the u32).  A workgroup counts tiles
+// [blockIdx.x * per, + per) of the padded layout, 16-B loads (4 records a lane),
+// and adds its counts to gh whenever its tiles enter a new bucket.
+template <int NT, int IT>
+__global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btile,
+                                                 const uint64_t* __restrict__ bstart, uint32_t nb, uint32_t per, int s0,
+                                                 int b0, int s1, int b1, uint64_t* __restrict__ gh) {
+    constexpr uint32_t kTileN = NT * IT;
+    static_assert(IT % 4 == 0, "16-B loads");
+    __shared__ uint32_t c0[kRadix], c1[kRadix];
+    const uint32_t t = threadIdx.x;
+    const uint32_t m0 = (1u << b0) - 1u, m1 = (1u << b1) - 1u;
+    const uint32_t all = btile[nb];
+    uint32_t tile = blockIdx.x * per;
+    const uint32_t tend = tile + per < all ? tile + per : all;
+    if (tile >= tend) return;
+    for (uint32_t i = t; i < kRadix; i += NT) c0[i] = c1[i] = 0;
+    // bucket of the first tile: the last h with btile[h] <= tile (empty buckets share a start)
+    uint32_t lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (btile[mid] <= tile) lo = mid;
+        else hi = mid - 1;
+    }
+    uint32_t h = lo;
+    auto flush = [&]() {
+        __syncthreads();
+        for (uint32_t d = t; d < kRadix; d += NT) {
+            if (c0[d]) atomicAdd((unsigned long long*)&gh[(2ull * h) * kRadix + d], (unsigned long long)c0[d]);
+            if (c1[d]) atomicAdd((unsigned long long*)&gh[(2ull * h + 1) * kRadix + d], (unsigned long long)c1[d]);
+            c0[d] = c1[d] = 0;
+        }
+        __syncthreads();
+    };
+    __syncthreads();
+    for (; tile < tend; tile++) {
+        if (tile >= btile[h + 1]) {  // (workgroup-uniform) the tiles entered a later bucket
+            flush();
+            while (tile >= btile[h + 1]) h++;
+        }
+        const uint64_t tb = (uint64_t)tile * kTileN;
+        const uint64_t vend = (uint64_t)btile[h] * kTileN + (bstart[h + 1] - bstart[h]);
+#pragma unroll
+        for (int k = 0; k < IT / 4; k++) {
+            const uint64_t idx = tb + 4ull * ((uint64_t)k * NT + t);
+            if (idx >= vend) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(rec + idx);
+            const uint32_t r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (idx + q < vend) {
+                    atomicAdd(&c0[(r[q] >> s0) & m0], 1u);
+                    atomicAdd(&c1[(r[q] >> s1) & m1], 1u);
+                }
+        }
+    }
+    flush();
+}
+
+// One LSD pass inside the buckets of the packed layout (k_onesweep's
+// decoupled look-back, per bucket): tile = ticket; its bucket h (btile); the
+// records [btile[h] * tile, + count of h) are valid; the look-back stops at
+// the bucket's first tile, which publishes an inclusive prefix at once.
+// Digit d of bucket h starts at obase + dbase[h * dstride + d] (obase = the
+// bucket's padded start for u32 output; its dense start for kOut64, which
+// writes (h << lowbits | rec >> pack_f) << 32 | (rec & id mask)).
+// (launch bound of 4 waves per SIMD: without it the compiler spent 256 VGPRs
+// with spills, one workgroup per CU, 2.4x slower than k_onesweep)
+template <int NT, int IT, bool kOut64, int kLbPer = 2>
+__global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout32,
+                                                     uint64_t* __restrict__ kout64, const uint32_t* __restrict__ btile,
+                                                     const uint64_t* __restrict__ bstart, uint32_t nb, int shift,
+                                                     int dbits, const uint64_t* __restrict__ dbase, uint32_t dstride,
+                                                     int pack_f, int lowbits, uint64_t* __restrict__ status,
+                                                     uint32_t* __restrict__ ticket, uint64_t epoch,
+                                                     unsigned long long* __restrict__ err) {
+    constexpr int NW = NT / 64;
+    constexpr int kTileN = NT * IT;
+    constexpr int kDW = kRadix / 64;
+    static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
+    __shared__ uint32_t s_keys[kTileN];
+    __shared__ uint32_t s_wcnt[NW][kRadix];
+    __shared__ uint32_t s_tstart[kRadix];
+    __shared__ uint64_t s_run[kRadix];
+    __shared__ uint64_t s_scan[kDW];
+    __shared__ uint32_t s_tot[kRadix];
+    __shared__ uint32_t s_tile, s_h;
+
+    const int w = wave_id(), l = lane_id(), t = threadIdx.x;
+    const uint32_t ndig = 1u << dbits, dmask = ndig - 1u;
+    const bool digit_thread = t < (int)ndig;
+    if (t == 0) {
+        const uint32_t tl = atomicAdd(ticket, 1u);
+        s_tile = tl;
+        uint32_t lo = 0, hi = nb - 1;  // the last bucket starting at or before the tile
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (btile[mid] <= tl) lo = mid;
+            else hi = mid - 1;
+        }
+        s_h = lo;
+    }
+    if (t < kRadix) {
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) s_wcnt[ww][t] = 0;
+    }
+    __syncthreads();
+    // tile and bucket read with readfirstlane: wave-uniform (scalar) values, so the bucket's bounds
+    // and every per-item bound compare stay in SGPRs (read from LDS they spilled 256 VGPRs)
+    const uint64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
+    if (tile >= btile[nb]) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(s_h);
+    const uint64_t tile0 = btile[h];
+    const uint64_t tb = tile * kTileN;
+    const uint64_t vend = tile0 * kTileN + (bstart[h + 1] - bstart[h]);
+    const uint64_t lt = lanemask_lt();
+    const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
+    uint32_t key[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const uint64_t idx = wbase + (uint64_t)k * 64;
+        key[k] = idx < vend ? kin[idx] : ~0u;
+    }
+    uint32_t info[IT];  // as k_onesweep: rank in the item's group | group size << 8 | leader lane << 16
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const bool valid = wbase + (uint64_t)k * 64 < vend;
+        const uint32_t d = (key[k] >> shift) & dmask;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; b++) {
+            if (b < dbits) {
+                const bool bit = (d >> b) & 1;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+        }
+        info[k] = valid ? (uint32_t)__popcll(m & lt) | ((uint32_t)__popcll(m) << 8) | ((uint32_t)__builtin_ctzll(m) << 16)
+                        : 0xFFFFFFFFu;
+    }
+    uint32_t before[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        before[k] = 0;
+        if ((info[k] & 0xFFu) == 0u) before[k] = atomicAdd(&s_wcnt[w][(key[k] >> shift) & dmask], (info[k] >> 8) & 0xFFu);
+    }
+    uint32_t rank[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+        rank[k] = (uint32_t)__shfl((int)before[k], (int)((info[k] >> 16) & 63u), 64) + (info[k] & 0xFFu);
+    __syncthreads();
+    uint32_t cw[NW];
+    uint32_t tot_d = 0;
+    if (t < kRadix) {
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            cw[ww] = s_wcnt[ww][t];
+            tot_d += cw[ww];
+        }
+    }
+    const uint64_t ep = epoch << 40;
+    if (digit_thread) {
+        s_tot[t] = tot_d;
+        __hip_atomic_store(status + tile * kRadix + t, ep | (tile == tile0 ? kLbFlagP : kLbFlagA) | tot_d,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t inc = wave_incl_scan(tot_d);
+    if (w < kDW && l == 63) s_scan[w] = inc;
+    __syncthreads();
+    uint64_t wb = 0, all = 0;
+#pragma unroll
+    for (int ww = 0; ww < kDW; ww++) {
+        const uint64_t sv = s_scan[ww];
+        if (ww < w) wb += sv;
+        all += sv;
+    }
+    if (t < kRadix) {
+        uint32_t run = (uint32_t)(wb + inc - tot_d);
+        s_tstart[t] = run;
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            s_wcnt[ww][t] = run;
+            run += cw[ww];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        if (wbase + (uint64_t)k * 64 < vend) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
+    }
+    // look-back over the bucket's earlier tiles (k_onesweep's quads of lanes)
+    const uint64_t obase = kOut64 ? bstart[h] : tile0 * kTileN;
+    const uint32_t gj = t & 3;
+    for (uint32_t gd = t >> 2; gd < ndig; gd += NT / 4) {
+        uint64_t excl = 0;
+        for (int64_t base = (int64_t)tile - 1; base >= (int64_t)tile0; base -= 4 * kLbPer) {
+            uint64_t v[kLbPer];
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++) {
+                const int64_t p = base - (int64_t)(4 * u + gj);
+                v[u] = p >= (int64_t)tile0 ? __hip_atomic_load(status + (uint64_t)p * kRadix + gd, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)
+                                           : ep | kLbFlagP;  // before the bucket's first tile: a prefix of 0
+            }
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++) {
+                const int64_t p = base - (int64_t)(4 * u + gj);
+                for (uint32_t spin = 0; (v[u] >> 40) != epoch; spin++) {
+                    if (spin == (1u << 24)) {
+                        atomicOr(err, kLbTimeout);
+                        v[u] = ep | kLbFlagP;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    v[u] = __hip_atomic_load(status + (uint64_t)p * kRadix + gd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            uint32_t q = 0;
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++)
+                q |= ((uint32_t)(__ballot((v[u] & kLbFlagP) != 0) >> (lane_id() & ~3)) & 0xFu) << (4 * u);
+            const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 4u * kLbPer - 1u;
+            uint64_t add = 0;
+#pragma unroll
+            for (int u = 0; u < kLbPer; u++)
+                if (4u * u + gj <= upto) add += v[u] & kLbValMask;
+            add += (uint64_t)__shfl_xor((long long)add, 1, 64);
+            add += (uint64_t)__shfl_xor((long long)add, 2, 64);
+            excl += add;
+            if (q) break;
+        }
+        if (gj == 0) {
+            if (tile != tile0)
+                __hip_atomic_store(status + tile * kRadix + gd, ep | kLbFlagP | (excl + s_tot[gd]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_run[gd] = obase + dbase[(uint64_t)h * dstride + gd] + excl;
+        }
+    }
+    __syncthreads();
+    const uint32_t tile_n = (uint32_t)all;
+    const uint32_t idmask = (1u << pack_f) - 1u;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        const uint32_t p = j * NT + t;
+        if (p < tile_n) {
+            const uint32_t k = s_keys[p];
+            const uint32_t d = (k >> shift) & dmask;
+            const uint64_t dst = s_run[d] + (p - s_tstart[d]);
+            if (kOut64) kout64[dst] = ((uint64_t)((h << lowbits) | (k >> pack_f)) << 32) | (k & idmask);
+            else kout32[dst] = k;
         }
     }
 }

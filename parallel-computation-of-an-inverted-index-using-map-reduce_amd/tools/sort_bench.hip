@@ -356,7 +356,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(table, ht.data(), ht.size() * 8, hipMemcpyHostToDevice));
         const float ts = time_best([&] {
             k_radix_scatter<false, kScatterThreads, kScatterItems><<<nch, kScatterThreads>>>(
-                a, b, nullptr, nullptr, n, chunk, shift, dbits, nch, table, nullptr);
+                a, b, nullptr, nullptr, n, chunk, shift, dbits, nch, table, nullptr, nullptr, nullptr, 0, 0u);
         });
         CK(hipMemset(bad, 0, 8));
         k_check_sorted<<<4096, 256>>>(b, n, shift, (1u << dbits) - 1, bad);

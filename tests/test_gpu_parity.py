@@ -379,3 +379,28 @@ def test_large_vocab_vs_oracle_both_key_modes():
     finally:
         os.environ.pop("II_SORT_KEYS", None)
         ix.close()
+
+
+def test_packed_sort_forms_vs_oracle():
+    """The token sort's packed form (ii_prims.h "Packed token sort": MSD buckets
+    of u32 records, two bucket-local onesweep passes) against the u64 form
+    (II_PACKED_SORT=0) and the oracle: 7-bit top digit (ids of 10 bits), 8-bit
+    top digit (ids spread to 19 bits: W + F - 32 = 8) and ids too wide to pack
+    (22 bits: the u64 form runs)."""
+    t, off = ii_ctypes.zipf_corpus(48_000_000, 700, 300_000, 23, threads=8)
+    off = off.tolist()
+    for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 0)]:
+        exp = oracle_index(t, off, ids)
+        for env in [None, "0"]:
+            if env is not None:
+                os.environ["II_PACKED_SORT"] = env
+            try:
+                with ii_ctypes.Index(0) as ix:
+                    ix.map_host(t, off, ids)
+                    ix.reduce()
+                    assert_same(ix.letters(), exp, "ids up to %d, II_PACKED_SORT=%s" % (ids[-1], env))
+                    st = ix.stats()
+                    assert st.sort_packed == (packed if env is None else 0)
+                    assert st.sort_bytes > 0
+            finally:
+                os.environ.pop("II_PACKED_SORT", None)
