@@ -397,12 +397,17 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+// Inclusive wave64 scan with DPP (GFX9 row_shr inside the 16-lane rows, then
+// row_bcast:15 / :31 across them): six VALU adds instead of six ds_bpermute
+// round trips.  A lane whose source lies outside its row (or a row that the
+// row mask leaves out) adds the `old` operand, 0.
 __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
-        if (lane_id() >= o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -583,10 +588,10 @@ __device__ __forceinline__ void store_round(uint8_t* s_text, RoundRegs r, uint64
 
 // 4 letters (bytes, first in the low byte) -> their 5-bit codes, first letter
 // in the high bits (20 bits).  x & 0x1F is the letter code for A-Z and a-z.
+// Two v_dot4_u32_u8 of the codes: 32 c0 + c1 and 32 c2 + c3.
 __device__ __forceinline__ uint32_t pack4(uint32_t x) {
-    uint32_t r = __builtin_bswap32(x & 0x1F1F1F1Fu);            // b0@24 b1@16 b2@8 b3@0
-    r = (r & 0x001F001Fu) | ((r >> 3) & 0x03E003E0u);           // b0@21 b1@16 b2@5 b3@0
-    return (r & 0x3FFu) | ((r >> 6) & 0xFFC00u);                // b0@15 b1@10 b2@5 b3@0
+    const uint32_t c = x & 0x1F1F1F1Fu;
+    return (__builtin_amdgcn_udot4(c, 0x00000120u, 0u, false) << 10) | __builtin_amdgcn_udot4(c, 0x01200000u, 0u, false);
 }
 
 // Byte g (0..15) of the 16-byte value lo | hi << 64 removed: the bytes above
@@ -881,7 +886,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restric
         // 2. token index of every kept start (window j of all lanes before j + 1)
         const uint32_t inc = wave_incl_scan32(cnt);
         const uint32_t ex = inc - cnt;
-        const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         const uint32_t ntok = (tot & 0xFFFFu) + (tot >> 16);
         {
             uint32_t o = ex & 0xFFFFu;
