@@ -442,7 +442,8 @@ def main():
         T, Tk, U, V = st.tokens, st.sorted_records, st.pairs, st.words
         sp = max(1, st.sort_passes)
         survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
-        impl_b = 8 * T + 8 * Tk + st.sort_bytes + 8 * Tk + 8 * U + 8 * (V + U // 64) + 16 * V
+        k3_read = (4 if st.sort_packed else 8) * Tk  # the packed form's K3 reads u32 records
+        impl_b = 8 * T + 8 * Tk + st.sort_bytes + k3_read + 8 * U + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_gbs = survey_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         cpu = None

@@ -65,6 +65,7 @@ struct ii_ctx {
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
     DBuf msd;                    // packed token sort: bucket geometry, per-bucket digit counts and bases
+    DBuf tbk;                    // packed token sort: bucket of every tile (u16)
     uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
     uint64_t lb_epoch = 0;       // epoch of the last onesweep pass
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
@@ -103,6 +104,9 @@ struct ii_ctx {
     uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
     bool sort_packed = false;  // the last token sort ran in the packed form (run_sort_packed)
     uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
+    // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
+    uint32_t pk_nb = 0, pk_ntb = 0;
+    int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
     uint64_t nch_map = 0;   // K1b chunks of the last map
@@ -163,7 +167,8 @@ static inline double now_ms() {
 }
 static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 // bytes the packed token sort's u32 layout of n records may take (every bucket padded to whole tiles)
-static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)kRadix * kSweepTile); }
+// (n + (kRadix + 1) tiles: every bucket's last tile padded, plus the launch's whole tiles, k_onesweep_seg ncap)
+static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
 static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
@@ -448,9 +453,16 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     // per-bucket digit counts of the two LSD passes -> bases
     c->sort_packed = true;
     c->sort_hist_bytes = 4 * n;
+    c->pk_nb = nb;
+    c->pk_F = F;
+    c->pk_L = L;
     const uint64_t ntb = (n + kSweepTile - 1) / kSweepTile + nb;  // tiles of the padded layout, at most
     const uint32_t hg = (uint32_t)std::min<uint64_t>(kMaxChunks, ntb);
     const uint32_t per = (uint32_t)((ntb + hg - 1) / hg);
+    c->pk_ntb = (uint32_t)ntb;
+    CK(grow(c->tbk, sizeof(uint16_t) * ntb));
+    uint16_t* tbk = P_<uint16_t>(c->tbk);
+    k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
     k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
         reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
@@ -460,17 +472,14 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
         CK(lookback_pass(c, ntb * kRadix));
         const bool evp = c->n_sc < kMaxTimedPasses;
         if (evp) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        if (p == 0)
-            k_onesweep_seg<kSweepThreads, kSweepItems, false><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
-                reinterpret_cast<const uint32_t*>(*k), reinterpret_cast<uint32_t*>(*k2), nullptr, btile, bstart, nb, F,
-                b0, gbase, 2 * kRadix, F, L, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err);
-        else
-            k_onesweep_seg<kSweepThreads, kSweepItems, true><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
-                reinterpret_cast<const uint32_t*>(*k2), nullptr, *k, btile, bstart, nb, F + b0, b1, gbase + kRadix,
-                2 * kRadix, F, L, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err);
+        k_onesweep_seg<kSweepThreads, kSweepItems><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+            reinterpret_cast<const uint32_t*>(p == 0 ? *k : *k2), ntb * kSweepTile,
+            reinterpret_cast<uint32_t*>(p == 0 ? *k2 : *k), btile,
+            tbk, bstart, nb, p == 0 ? F : F + b0, p == 0 ? b0 : b1, gbase + p * kRadix, 2 * kRadix, P_<uint64_t>(c->lbstat),
+            P_<uint32_t>(c->ticket), c->lb_epoch, err);
         if (evp) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
-            c->sc_bytes[c->n_sc++] = p == 0 ? 8 * n : 12 * n;
+            c->sc_bytes[c->n_sc++] = 8 * n;
         }
         HIPCK(hipGetLastError());
         (*passes)++;
@@ -481,7 +490,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
 // K3: distinct (lexid, id0) pairs of the sorted records r[0, n), their
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
 // (post_start[V] = U).  Sets c->U.
-static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false) {
+static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed) {
     c->xpairs = false;
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
@@ -507,12 +516,23 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid = false
         pe_k = P_<uint64_t>(c->pstop_w);
     }
     // one pass with decoupled look-back (k_uniq_sweep): U -> post_start[V], posting bytes -> totals[6]
-    const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
-    CK(lookback_pass(c, 2 * ntiles));
-    k_uniq_sweep<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(r, n, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
-                                                         P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-                                                         P_<unsigned long long>(c->counters) + C_OVERFLOW);
-    k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
+    if (packed) {  // r: the packed sort's u32 records in their padded buckets (k_uniq_sweep<true>)
+        const uint64_t* bstart = P_<uint64_t>(c->msd);
+        const uint32_t* btile = reinterpret_cast<const uint32_t*>(bstart + 2 * kRadix + 1);
+        const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
+        CK(lookback_pass(c, 2 * ntiles));
+        k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
+            nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
+            pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
+            P_<unsigned long long>(c->counters) + C_OVERFLOW);
+    } else {
+        const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
+        CK(lookback_pass(c, 2 * ntiles));
+        k_uniq_sweep<false><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
+            r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
+            P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW);
+        k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
+    }
     if (wid)
         k_wid_post<<<grid_for(c->V), kBlock, 0, c->st>>>(P_<uint32_t>(c->widl), (uint32_t)c->V, ps_k, pe_k, ps, pe);
     HIPCK(hipGetLastError());
@@ -1167,7 +1187,7 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     }
 
     // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
-    CK(run_unique(c, r, Tk, wid));
+    CK(run_unique(c, r, Tk, wid, c->sort_packed));
     c->wid_pairs = wid;
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;
@@ -1484,7 +1504,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
-    CK(run_unique(c, r, NP));
+    CK(run_unique(c, r, NP, false, false));  // the owner's merged pairs: dense u64 records
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)(p1 + p2);
     c->have_pairs = true;

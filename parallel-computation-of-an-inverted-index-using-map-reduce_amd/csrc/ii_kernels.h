@@ -1529,36 +1529,6 @@ __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
            (v >= 1000000ull) + (v >= 10000000ull) + (v >= 100000000ull) + (v >= 1000000000ull);
 }
 
-// The thread's records of the tile at base (loads only; lane 0 also loads the
-// record before each of its items, the other lanes take it from a neighbour).
-struct UniqTile {
-    uint64_t r[kUniqItems], p0[kUniqItems];
-};
-__device__ __forceinline__ void uniq_load(const uint64_t* __restrict__ rec, uint64_t base, uint64_t hi, UniqTile& u) {
-#pragma unroll
-    for (int q = 0; q < kUniqItems; q++) {
-        const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
-        u.r[q] = i < hi ? rec[i] : ~0ull;
-        u.p0[q] = (lane_id() == 0 && i > 0 && i <= hi) ? rec[i - 1] : ~0ull;
-    }
-}
-// Per item, whether it starts a distinct pair (1 in the 16-bit field q of
-// cnt) and its posting bytes (field q of bytes); prev[q] = the record before.
-__device__ __forceinline__ void uniq_eval(const UniqTile& u, uint64_t base, uint64_t hi, uint64_t (&prev)[kUniqItems],
-                                          uint64_t& cnt, uint64_t& bytes) {
-    cnt = bytes = 0;
-#pragma unroll
-    for (int q = 0; q < kUniqItems; q++) {
-        const uint64_t i = base + (uint64_t)q * kBlock + threadIdx.x;
-        uint64_t pv = (uint64_t)__shfl_up((long long)u.r[q], 1, 64);
-        if (lane_id() == 0) pv = u.p0[q];
-        prev[q] = pv;
-        if (i < hi && (i == 0 || u.r[q] != pv)) {
-            cnt |= 1ull << (16 * q);
-            bytes += (uint64_t)(id_digits((u.r[q] & 0xFFFFFFFFull) + 1) + 1) << (16 * q);
-        }
-    }
-}
 __device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
     return (x & 0xFFFFull) + ((x >> 16) & 0xFFFFull) + ((x >> 32) & 0xFFFFull) + (x >> 48);
 }
@@ -1573,8 +1543,21 @@ __device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
 // *U_out = distinct pairs, *B_out = posting bytes.
 constexpr int kUniqSub = 4;  // 1, 2, 8 sub-tiles: 5.65, 3.51, 4.83 ms against 2.94 at 10 GB (ticket rate, occupancy)
 constexpr int kUniqSweepTile = kUniqSub * kUniqTile;  // 4096 records
+// kPacked: the records come from the packed token sort (k_onesweep_seg, u32
+// low << pack_f | id in tile-padded buckets, ii_prims.h): K3 tile `tile` lies
+// in sort tile tile / 2, so in one bucket h; its valid records end at the
+// bucket's count, the word id is h << lowbits | low, and the first record of a
+// bucket has no predecessor (a bucket's words differ from every other
+// bucket's).  The last record of each bucket closes its word (post_end),
+// which the dense form leaves to the next word's start and k_post_last.
+static_assert(kSweepTile == 2 * kUniqSweepTile, "K3 tile = half a packed-sort tile");
+template <bool kPacked>
 __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
-                                                       uint64_t* __restrict__ uniq, uint64_t* __restrict__ P,
+                                                       const uint32_t* __restrict__ rec32, uint64_t ncap,
+                                                       const uint32_t* __restrict__ btile,
+                                                       const uint16_t* __restrict__ tbk,
+                                                       const uint64_t* __restrict__ bstart, uint32_t nb, int pack_f,
+                                                       int lowbits, uint64_t* __restrict__ uniq, uint64_t* __restrict__ P,
                                                        uint64_t* __restrict__ post_start, uint64_t* __restrict__ post_end,
                                                        uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
@@ -1585,24 +1568,54 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
     __shared__ uint64_t s_tot[kUniqSub][2];         // per sub-tile: pair / byte totals (16-bit fields)
     __shared__ uint64_t s_base[2];
     __shared__ uint32_t s_tile;
+    constexpr int kPer = kUniqSweepTile / kBlock;
     const int t = threadIdx.x;
     if (t == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint64_t tile = s_tile;
-    const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
-    const uint64_t lo = tile * kUniqSweepTile, hi = lo + kUniqSweepTile < n ? lo + kUniqSweepTile : n;
-    // the tile (and the record before it) staged in LDS: scanned, then written after the look-back
-    {
-        uint64_t v[kUniqSweepTile / kBlock];
+    const uint64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
+    const uint64_t lo = tile * kUniqSweepTile;
+    uint64_t ntiles, hi, first = 0, vend = 0;
+    uint64_t v[kPer];
+    uint64_t prev = ~0ull;  // the record before the tile (~0: none)
+    if (kPacked) {
+        // the loads first (their addresses do not depend on the bucket; ncap bounds the padded layout's
+        // allocation), the bucket's bounds while they are in flight: a chain of loads before them made
+        // the tiles publish late and K3 ran 1.6x longer
+        uint32_t raw[kPer];
 #pragma unroll
-        for (int j = 0; j < kUniqSweepTile / kBlock; j++) {
+        for (int j = 0; j < kPer; j++) {
+            const uint64_t i = lo + (uint64_t)j * kBlock + t;
+            raw[j] = i < ncap ? rec32[i] : 0u;
+        }
+        const uint32_t rprev = (t == 0 && lo > 0 && lo <= ncap) ? rec32[lo - 1] : 0u;
+        ntiles = 2ull * btile[nb];
+        if (tile >= ntiles) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
+        const uint32_t h = tbk[tile / 2];
+        first = (uint64_t)btile[h] * kSweepTile;
+        vend = first + (bstart[h + 1] - bstart[h]);
+        hi = lo + kUniqSweepTile < vend ? lo + kUniqSweepTile : vend;
+        hi = hi < lo ? lo : hi;
+        const uint32_t idmask = (1u << pack_f) - 1u;
+        auto unpack = [&](uint32_t x) -> uint64_t {
+            return ((uint64_t)((h << lowbits) | (x >> pack_f)) << 32) | (x & idmask);
+        };
+#pragma unroll
+        for (int j = 0; j < kPer; j++) v[j] = lo + (uint64_t)j * kBlock + t < hi ? unpack(raw[j]) : ~0ull;
+        if (lo > first && lo < vend) prev = unpack(rprev);
+    } else {
+        ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
+        hi = lo + kUniqSweepTile < n ? lo + kUniqSweepTile : n;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
             const uint64_t i = lo + (uint64_t)j * kBlock + t;
             v[j] = i < hi ? rec[i] : ~0ull;
         }
-#pragma unroll
-        for (int j = 0; j < kUniqSweepTile / kBlock; j++) s_rec[1 + j * kBlock + t] = v[j];
-        if (t == 0) s_rec[0] = lo > 0 ? rec[lo - 1] : ~0ull;
+        if (t == 0 && lo > 0) prev = rec[lo - 1];
     }
+    // the tile (and the record before it) staged in LDS: scanned, then written after the look-back
+#pragma unroll
+    for (int j = 0; j < kPer; j++) s_rec[1 + j * kBlock + t] = v[j];
+    if (t == 0) s_rec[0] = prev;
     __syncthreads();
     // item (k, q) of this thread: tile index k * kUniqTile + q * kBlock + t (coalesced)
     auto item = [&](int k, int q, uint64_t& r, uint64_t& pv) {
@@ -1619,7 +1632,7 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
             uint64_t r, pv;
             item(k, q, r, pv);
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
-            if (i < hi && (i == 0 || r != pv)) {
+            if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
                 c |= 1ull << (16 * q);
                 b += (uint64_t)(id_digits((r & 0xFFFFFFFFull) + 1) + 1) << (16 * q);
             }
@@ -1693,21 +1706,26 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
 #pragma unroll
         for (int q = 0; q < kUniqItems; q++) {
             const uint64_t f = (ec >> (16 * q)) & 0xFFFFull;
+            const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (f & 0x8000ull) {
                 uint64_t r, pv;
                 item(k, q, r, pv);
                 const uint64_t uu = rc + (f & 0x7FFFull);
                 const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
                 uniq[uu] = r;
-                const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
-                const bool wstart = i == 0 || key != pkey;
+                const bool wstart = pv == ~0ull || key != pkey;
                 // P is read at word starts (k_fmt_words, OpLineOff) and at the
                 // first posting of every 64 (k_fmt_posts) only
                 if (wstart || (uu & 63u) == 0) P[uu] = rb + ((eb >> (16 * q)) & 0xFFFFull);
                 if (wstart) {
                     post_start[key] = uu;
-                    if (i > 0) post_end[pkey] = uu;
+                    if (pv != ~0ull) post_end[pkey] = uu;
                 }
+            }
+            if (kPacked && i + 1 == vend) {  // the bucket's last record: its word ends after the pairs so far
+                uint64_t r, pv;
+                item(k, q, r, pv);
+                post_end[(uint32_t)(r >> 32)] = rc + (f & 0x7FFFull) + ((f >> 15) & 1u);
             }
             rc += (tc >> (16 * q)) & 0xFFFFull;
             rb += (tb >> (16 * q)) & 0xFFFFull;

@@ -583,9 +583,10 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
 // low << F | id (low = the key's other W - m bits): the bucket implies the top
 // digit.  The remaining digits are sorted inside each bucket by onesweep passes
 // over the u32 records (k_onesweep_seg): a tile lies in one bucket and looks
-// back only over its bucket's tiles.  The last pass writes the full u64
-// records at their dense places.  Against three u64 passes this moves 36
-// instead of 48 bytes per record (8 + 4 scatter, 4 histogram, 4 + 4, 4 + 8).
+// back only over its bucket's tiles.  K3 (k_uniq_sweep<true>) reads the
+// sorted u32 records in the same padded layout and writes the u64 pairs.
+// Against three u64 passes and a u64 K3 read this moves 36 instead of 56
+// bytes per record (8 + 4 scatter, 4 histogram, 4 + 4, 4 + 4, K3 read 4).
 //
 // Bucket geometry (one workgroup): bstart[h] = dense start of bucket h (the
 // exclusive scan of the MSD scatter's digit-major table, column 0) and
@@ -619,6 +620,13 @@ __global__ __launch_bounds__(kRadix) void k_msd_geometry(const uint64_t* __restr
         bstart[nb] = tot;
         btile[nb] = (uint32_t)all;
     }
+}
+
+// tbk[tile] = the bucket of every tile of the padded layout (one workgroup
+// per bucket), so that a tile finds its bucket with one load.
+__global__ __launch_bounds__(kBlock) void k_tile_buckets(const uint32_t* __restrict__ btile, uint16_t* __restrict__ tbk) {
+    const uint32_t h = blockIdx.x;
+    for (uint32_t i = btile[h] + threadIdx.x; i < btile[h + 1]; i += kBlock) tbk[i] = (uint16_t)h;
 }
 
 // Per-bucket counts of the two LSD digits of the packed records:
@@ -686,17 +694,17 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
 // decoupled look-back, per bucket): tile = ticket; its bucket h (btile); the
 // records [btile[h] * tile, + count of h) are valid; the look-back stops at
 // the bucket's first tile, which publishes an inclusive prefix at once.
-// Digit d of bucket h starts at obase + dbase[h * dstride + d] (obase = the
-// bucket's padded start for u32 output; its dense start for kOut64, which
-// writes (h << lowbits | rec >> pack_f) << 32 | (rec & id mask)).
+// Digit d of bucket h starts at the bucket's padded start + dbase[h * dstride + d].
 // (launch bound of 4 waves per SIMD: without it the compiler spent 256 VGPRs
 // with spills, one workgroup per CU, 2.4x slower than k_onesweep)
-template <int NT, int IT, bool kOut64, int kLbPer = 2>
-__global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout32,
-                                                     uint64_t* __restrict__ kout64, const uint32_t* __restrict__ btile,
+template <int NT, int IT, int kLbPer = 2>
+__global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,
+                                                     uint32_t* __restrict__ kout,
+                                                     const uint32_t* __restrict__ btile,
+                                                     const uint16_t* __restrict__ tbk,
                                                      const uint64_t* __restrict__ bstart, uint32_t nb, int shift,
                                                      int dbits, const uint64_t* __restrict__ dbase, uint32_t dstride,
-                                                     int pack_f, int lowbits, uint64_t* __restrict__ status,
+                                                     uint64_t* __restrict__ status,
                                                      uint32_t* __restrict__ ticket, uint64_t epoch,
                                                      unsigned long long* __restrict__ err) {
     constexpr int NW = NT / 64;
@@ -709,43 +717,38 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
     __shared__ uint64_t s_run[kRadix];
     __shared__ uint64_t s_scan[kDW];
     __shared__ uint32_t s_tot[kRadix];
-    __shared__ uint32_t s_tile, s_h;
+    __shared__ uint32_t s_tile;
 
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
     const uint32_t ndig = 1u << dbits, dmask = ndig - 1u;
     const bool digit_thread = t < (int)ndig;
-    if (t == 0) {
-        const uint32_t tl = atomicAdd(ticket, 1u);
-        s_tile = tl;
-        uint32_t lo = 0, hi = nb - 1;  // the last bucket starting at or before the tile
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) / 2;
-            if (btile[mid] <= tl) lo = mid;
-            else hi = mid - 1;
-        }
-        s_h = lo;
-    }
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
     if (t < kRadix) {
 #pragma unroll
         for (int ww = 0; ww < NW; ww++) s_wcnt[ww][t] = 0;
     }
     __syncthreads();
-    // tile and bucket read with readfirstlane: wave-uniform (scalar) values, so the bucket's bounds
-    // and every per-item bound compare stay in SGPRs (read from LDS they spilled 256 VGPRs)
+    // the tile read with readfirstlane: wave-uniform (scalar), so the bucket's bounds and every
+    // per-item bound compare stay in SGPRs (read from LDS they spilled 256 VGPRs)
     const uint64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
-    if (tile >= btile[nb]) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
-    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(s_h);
-    const uint64_t tile0 = btile[h];
     const uint64_t tb = tile * kTileN;
-    const uint64_t vend = tile0 * kTileN + (bstart[h + 1] - bstart[h]);
     const uint64_t lt = lanemask_lt();
     const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
+    // the keys first (their addresses do not depend on the bucket; ncap bounds the padded layout's
+    // allocation), the bucket's bounds while they are in flight
     uint32_t key[IT];
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const uint64_t idx = wbase + (uint64_t)k * 64;
-        key[k] = idx < vend ? kin[idx] : ~0u;
+        key[k] = idx < ncap ? kin[idx] : ~0u;
     }
+    if (tile >= btile[nb]) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
+    const uint32_t h = tbk[tile];
+    const uint64_t tile0 = btile[h];
+    const uint64_t vend = tile0 * kTileN + (bstart[h + 1] - bstart[h]);
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+        if (wbase + (uint64_t)k * 64 >= vend) key[k] = ~0u;
     uint32_t info[IT];  // as k_onesweep: rank in the item's group | group size << 8 | leader lane << 16
 #pragma unroll
     for (int k = 0; k < IT; k++) {
@@ -814,7 +817,7 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
         if (wbase + (uint64_t)k * 64 < vend) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
     }
     // look-back over the bucket's earlier tiles (k_onesweep's quads of lanes)
-    const uint64_t obase = kOut64 ? bstart[h] : tile0 * kTileN;
+    const uint64_t obase = tile0 * kTileN;
     const uint32_t gj = t & 3;
     for (uint32_t gd = t >> 2; gd < ndig; gd += NT / 4) {
         uint64_t excl = 0;
@@ -863,16 +866,12 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
     }
     __syncthreads();
     const uint32_t tile_n = (uint32_t)all;
-    const uint32_t idmask = (1u << pack_f) - 1u;
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         const uint32_t p = j * NT + t;
         if (p < tile_n) {
             const uint32_t k = s_keys[p];
-            const uint32_t d = (k >> shift) & dmask;
-            const uint64_t dst = s_run[d] + (p - s_tstart[d]);
-            if (kOut64) kout64[dst] = ((uint64_t)((h << lowbits) | (k >> pack_f)) << 32) | (k & idmask);
-            else kout32[dst] = k;
+            kout[s_run[(k >> shift) & dmask] + (p - s_tstart[(k >> shift) & dmask])] = k;
         }
     }
 }
