@@ -358,13 +358,15 @@ def main():
     if nbytes:
         d_text[:nbytes].copy_(torch.from_numpy(text[:nbytes]))
     torch.cuda.synchronize()
-    file_start = off[:-1].tolist()
+    # the file table as contiguous arrays: passed to ii_map_device in place every step
+    file_start = np.ascontiguousarray(off[:-1], dtype=np.uint64)
+    file_ids = np.ascontiguousarray(ids, dtype=np.uint32)
 
     idx = ii_ctypes.Index(local if world > 1 else 0)
     owned = [(0, 26)]
 
     def step(copy_text=False):
-        idx.map_device(d_text.data_ptr(), nbytes, file_start, ids)
+        idx.map_device(d_text.data_ptr(), nbytes, file_start, file_ids)
         if world > 1:  # local reduce -> letter-range all-to-allv (RCCL) -> owner merge + format
             _, (lo, hi) = ii_dist.exchange_and_reduce(idx, id_bound, balanced=a.letter_split == "balanced",
                                                       copy_text=copy_text)

@@ -8,6 +8,8 @@ missing: there is no CPU fallback.
 import ctypes
 import os
 
+import numpy as np
+
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALPHABET = 26
 
@@ -117,12 +119,21 @@ def _check(rc, what):
         raise IIError(rc, what)
 
 
+def _array(seq, ctype, dtype):
+    """A C array of seq: a contiguous numpy array of the right dtype is passed
+    in place (no per-call copy: a 10^5-entry file table took milliseconds to
+    marshal element by element), anything else is copied into a ctypes array."""
+    if isinstance(seq, np.ndarray) and seq.dtype == dtype and seq.flags.c_contiguous and len(seq):
+        return seq.ctypes.data_as(ctypes.POINTER(ctype))  # keeps a reference to seq
+    return (ctype * max(1, len(seq)))(*seq)
+
+
 def _u64(seq):
-    return (ctypes.c_uint64 * max(1, len(seq)))(*seq)
+    return _array(seq, ctypes.c_uint64, np.uint64)
 
 
 def _u32(seq):
-    return (ctypes.c_uint32 * max(1, len(seq)))(*seq)
+    return _array(seq, ctypes.c_uint32, np.uint32)
 
 
 class Index:

@@ -585,7 +585,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
-                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x};
+                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -680,22 +680,23 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     const uint64_t* fstart = P_<uint64_t>(c->fstart);
     const uint32_t* fid = P_<uint32_t>(c->fid);
 
-    k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, counters);
+    // the separator contract, checked on the device (totals[9]); the host looks once, with the map's
+    // other results
+    HIPCK(hipMemsetAsync(totals + 9, 0, sizeof(uint64_t), c->st));
+    k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, totals + 9);
     HIPCK(hipMemsetAsync(chunk_cnt + nch, 0, sizeof(uint64_t), c->st));  // voff[nch] = T after the scan
     c->rec_cap = use_fixed_capacity(c, nch, dense) ? kChunkCap : 0;
-    uint64_t hv[2];
     if (c->rec_cap) {
-        CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
-        if (hv[1] & 4) return II_ERR_LAYOUT;
         CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, packed_bytes(nch * kChunkCap))));
         CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
         c->T = 0;
     } else {
+        uint64_t hv[2];
         k_tok_count<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, chunk_cnt);
         CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
         CK(read_u64(c, totals, &hv[0]));
-        CK(read_u64(c, counters + C_OVERFLOW, &hv[1]));
-        if (hv[1] & 4) return II_ERR_LAYOUT;
+        CK(read_u64(c, totals + 9, &hv[1]));
+        if (hv[1]) return II_ERR_LAYOUT;
         c->T = hv[0];
         CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
         CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
@@ -708,6 +709,9 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;  // the long queue grows on overflow
     if (c->long_cap < std::max<uint64_t>(1 << 16, t_est / 64)) c->long_cap = std::max<uint64_t>(1 << 16, t_est / 64);
 
+    // K1b, its counts, the exactness check of hashed keys, the token count scan
+    // and the letter histogram are all queued before the host looks: one host
+    // round trip per attempt (a retry redoes them all)
     for (int attempt = 0;; attempt++) {
         if (attempt > 12) return II_ERR_INTERNAL;
         if (c->big_cap > (1ull << 30)) return II_ERR_NOMEM;  // slots must fit 31 bits
@@ -730,8 +734,18 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
-        uint64_t cnt[C_LONGMAX + 1];
-        CK(read_u64(c, counters, cnt, C_LONGMAX + 1));
+        HIPCK(hipEventRecord(c->ev_res[0], c->st));
+        k_long_verify<<<dim3(kLongShards, kLvBlocks), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs),
+                                                                         c->long_cap / kLongShards,
+                                                                         P_<uint64_t>(c->trep), counters);
+        HIPCK(hipEventRecord(c->ev_res[1], c->st));
+        if (c->rec_cap) CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));  // chunk token counts -> voff
+        k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
+        HIPCK(hipGetLastError());
+        uint64_t cnt[C_LONGMAX + 1], tot[10];  // (C_HIST .. C_HIST + 25 lie inside)
+        HIPCK(hipMemcpyAsync(cnt, counters, sizeof(cnt), hipMemcpyDeviceToHost, c->st));
+        CK(read_u64(c, totals, tot, 10));
+        if (tot[9]) return II_ERR_LAYOUT;
         if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] > kHotSlots / 2 + c->big_cap / 2) {
             c->big_cap *= 4;
             c->retries++;
@@ -742,34 +756,21 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
             c->retries++;
             continue;
         }
-        c->nlong = cnt[C_LONG];
-        if (c->nlong) {
-            const dim3 g(kLongShards, (uint32_t)std::min<uint64_t>(128, grid_for(cnt[C_LONGMAX])));
-            HIPCK(hipEventRecord(c->ev_res[0], c->st));
-            k_long_verify<<<g, kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs), c->long_cap / kLongShards,
-                                                 P_<uint64_t>(c->trep), counters);
-            HIPCK(hipEventRecord(c->ev_res[1], c->st));
-            HIPCK(hipGetLastError());
-            CK(read_u64(c, counters, cnt, 4));
-            if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
-                c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
-                c->retries++;
-                continue;
-            }
+        if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
+            c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
+            c->retries++;
+            continue;
         }
+        c->nlong = cnt[C_LONG];
         c->V = cnt[C_INSERT];
-        CK(read_u64(c, totals + 5, &c->n_pending));
+        c->n_pending = tot[5];
+        if (c->rec_cap) {
+            c->T = tot[0];
+            CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
+        }
+        memcpy(c->hist, cnt + C_HIST, sizeof(c->hist));
         break;
     }
-    if (c->rec_cap) {  // chunk token counts -> voff (exclusive scan, voff[nch] = T)
-        CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));
-        CK(read_u64(c, totals, &c->T));
-        CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
-    }
-    HIPCK(hipMemsetAsync(counters + C_HIST, 0, sizeof(uint64_t) * II_ALPHABET, c->st));
-    k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
-    HIPCK(hipGetLastError());
-    CK(read_u64(c, counters + C_HIST, c->hist, II_ALPHABET));
     if (hist_out) memcpy(hist_out, c->hist, sizeof(c->hist));
     HIPCK(hipEventRecord(c->ev[1], c->st));
     c->mapped = true;

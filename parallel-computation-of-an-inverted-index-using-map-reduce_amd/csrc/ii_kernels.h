@@ -1070,6 +1070,9 @@ __device__ __forceinline__ int same_raw_token(const uint8_t* __restrict__ text, 
     return 0;
 }
 
+constexpr uint32_t kLvBlocks = 128;  // k_long_verify workgroups per queue shard (launched before the counts are known)
+static_assert(C_HIST + 26 <= C_LONGMAX, "map_core reads counters [0, C_LONGMAX]");
+
 // Exactness check for hashed keys: every long token must spell the same word
 // as its slot's representative occurrence.  Most occurrences repeat the
 // representative's bytes (same_raw_token); the rest are walked letter by letter.
@@ -1077,7 +1080,9 @@ __device__ __forceinline__ int same_raw_token(const uint8_t* __restrict__ text, 
 __global__ __launch_bounds__(kBlock) void k_long_verify(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                         const LongTok* __restrict__ longs, uint64_t long_per,
                                                         const uint64_t* __restrict__ rep, uint64_t* counters) {
-    const uint64_t n = counters[C_LSHARD + 16 * blockIdx.x];
+    // (the shard's count, at most its capacity: the queue may have overflowed, C_OVERFLOW bit 2, and the
+    // map retries then; the kernel is launched before the host has looked)
+    const uint64_t n = min((unsigned long long)counters[C_LSHARD + 16 * blockIdx.x], (unsigned long long)long_per);
     const LongTok* q = longs + blockIdx.x * long_per;
     for (uint64_t i = (uint64_t)blockIdx.y * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.y * kBlock) {
         LongTok lt = q[i];
@@ -1114,13 +1119,14 @@ __global__ void k_long_totals(uint64_t* counters) {
 }
 static_assert(kLongShards == 64, "k_long_totals: one lane per shard");
 
-// Separator contract of ii_map_device: the byte before every file start is whitespace.
+// Separator contract of ii_map_device: the byte before every file start is
+// whitespace (*bad != 0 otherwise).
 __global__ void k_check_layout(const uint8_t* __restrict__ text, const uint64_t* __restrict__ file_start, uint32_t nfiles,
-                               uint64_t* counters) {
+                               uint64_t* bad) {
     uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f == 0 || f >= nfiles) return;
     uint64_t s = file_start[f];
-    if (s > 0 && !is_ws(text[s - 1])) atomicOr((unsigned long long*)&counters[C_OVERFLOW], 4ull);
+    if (s > 0 && !is_ws(text[s - 1])) atomicOr((unsigned long long*)bad, 1ull);
 }
 
 // ---------------------------------------------------------------- dictionary
