@@ -6,7 +6,11 @@ steps ii_dist.exchange_and_reduce runs per rank — local reduce, plan +
 export, the exchange (device copies here; RCCL all-to-allv on a node),
 import, order + format — each timed across all G contexts.
 
-    python tools/exchange_timing.py [bytes_per_shard] [G] [steps]
+    python tools/exchange_timing.py [bytes_per_shard] [G] [steps] [interleaved]
+
+interleaved = 1: shard g owns files g, g + G, g + 2G, ... (the id ranges of
+the sources overlap, as with bench.py's ii_partition shards, so the owners
+sort their merged pairs instead of merging ordered runs).
 """
 import json
 import os
@@ -26,13 +30,15 @@ def main():
     nb = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(2e9)
     G = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    inter = len(sys.argv) > 4 and sys.argv[4] == "1"
     files = 2000
     texts = []
     for g in range(G):
         t, off = ii_ctypes.zipf_corpus(nb, files, 1_000_000, 3 + 1000 * g, threads=16)
         d = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
         d[:nb].copy_(torch.from_numpy(t))
-        texts.append((d, off[:-1].tolist(), list(range(g * files, (g + 1) * files))))
+        ids = list(range(g, G * files, G)) if inter else list(range(g * files, (g + 1) * files))
+        texts.append((d, off[:-1].tolist(), ids))
     torch.cuda.synchronize()
     idxs = [ii_ctypes.Index(0) for _ in range(G)]
     res = []
@@ -82,7 +88,7 @@ def main():
             res.append(ph)
     avg = {k: round(sum(r[k] for r in res) / len(res), 2) for k in res[0]}
     avg["per_shard_ms"] = {k: round(v / G, 2) for k, v in avg.items() if k != "exchange_bytes"}
-    print(json.dumps({"G": G, "bytes_per_shard": nb, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
+    print(json.dumps({"G": G, "bytes_per_shard": nb, "interleaved_ids": inter, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
                       "phases_ms_all_shards": avg}))
     for ix in idxs:
         ix.close()
