@@ -1558,7 +1558,7 @@ constexpr int kUniqSweepTile = kUniqSub * kUniqTile;  // 4096 records
 // which the dense form leaves to the next word's start and k_post_last.
 static_assert(kSweepTile == 2 * kUniqSweepTile, "K3 tile = half a packed-sort tile");
 template <bool kPacked>
-__global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
+__global__ __launch_bounds__(kBlock, 8) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
                                                        const uint32_t* __restrict__ rec32, uint64_t ncap,
                                                        const uint32_t* __restrict__ btile,
                                                        const uint16_t* __restrict__ tbk,
@@ -1568,10 +1568,15 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
                                                        uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
                                                        uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err) {
-    __shared__ uint64_t s_rec[kUniqSweepTile + 1];  // [0]: the record before the tile; the tile from [1]
+    // the tile staged in LDS (scanned, then written after the look-back): u64
+    // records from [1] with the record before the tile at [0], or in the packed
+    // form the raw u32 records (16 KiB, 8 workgroups per CU instead of 3) and
+    // the record before the tile apart
+    __shared__ uint64_t s_rec[kPacked ? 1 : kUniqSweepTile + 1];
+    __shared__ uint32_t s_raw[kPacked ? kUniqSweepTile : 1];
+    __shared__ uint64_t s_prev;
     __shared__ uint64_t lds[2 * kWaves];
-    __shared__ uint64_t s_ex[kUniqSub][2][kBlock];  // per sub-tile and thread: exclusive pair / byte offsets (16-bit fields)
-    __shared__ uint64_t s_tot[kUniqSub][2];         // per sub-tile: pair / byte totals (16-bit fields)
+    __shared__ uint64_t s_tot[kUniqSub][2];  // per sub-tile: pair / byte totals (16-bit fields)
     __shared__ uint64_t s_base[2];
     __shared__ uint32_t s_tile;
     constexpr int kPer = kUniqSweepTile / kBlock;
@@ -1581,8 +1586,11 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
     const uint64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
     const uint64_t lo = tile * kUniqSweepTile;
     uint64_t ntiles, hi, first = 0, vend = 0;
-    uint64_t v[kPer];
-    uint64_t prev = ~0ull;  // the record before the tile (~0: none)
+    uint32_t h = 0;
+    const uint32_t idmask = kPacked ? (1u << pack_f) - 1u : 0u;
+    auto unpack = [&](uint32_t x) -> uint64_t {
+        return ((uint64_t)((h << lowbits) | (x >> pack_f)) << 32) | (x & idmask);
+    };
     if (kPacked) {
         // the loads first (their addresses do not depend on the bucket; ncap bounds the padded layout's
         // allocation), the bucket's bounds while they are in flight: a chain of loads before them made
@@ -1596,40 +1604,47 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
         const uint32_t rprev = (t == 0 && lo > 0 && lo <= ncap) ? rec32[lo - 1] : 0u;
         ntiles = 2ull * btile[nb];
         if (tile >= ntiles) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
-        const uint32_t h = tbk[tile / 2];
+        h = (uint32_t)__builtin_amdgcn_readfirstlane(tbk[tile / 2]);
         first = (uint64_t)btile[h] * kSweepTile;
         vend = first + (bstart[h + 1] - bstart[h]);
         hi = lo + kUniqSweepTile < vend ? lo + kUniqSweepTile : vend;
         hi = hi < lo ? lo : hi;
-        const uint32_t idmask = (1u << pack_f) - 1u;
-        auto unpack = [&](uint32_t x) -> uint64_t {
-            return ((uint64_t)((h << lowbits) | (x >> pack_f)) << 32) | (x & idmask);
-        };
 #pragma unroll
-        for (int j = 0; j < kPer; j++) v[j] = lo + (uint64_t)j * kBlock + t < hi ? unpack(raw[j]) : ~0ull;
-        if (lo > first && lo < vend) prev = unpack(rprev);
+        for (int j = 0; j < kPer; j++) s_raw[j * kBlock + t] = raw[j];
+        if (t == 0) s_prev = (lo > first && lo < vend) ? unpack(rprev) : ~0ull;
     } else {
         ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         hi = lo + kUniqSweepTile < n ? lo + kUniqSweepTile : n;
+        uint64_t v[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint64_t i = lo + (uint64_t)j * kBlock + t;
             v[j] = i < hi ? rec[i] : ~0ull;
         }
-        if (t == 0 && lo > 0) prev = rec[lo - 1];
-    }
-    // the tile (and the record before it) staged in LDS: scanned, then written after the look-back
 #pragma unroll
-    for (int j = 0; j < kPer; j++) s_rec[1 + j * kBlock + t] = v[j];
-    if (t == 0) s_rec[0] = prev;
+        for (int j = 0; j < kPer; j++) s_rec[1 + j * kBlock + t] = v[j];
+        if (t == 0) s_rec[0] = lo > 0 ? rec[lo - 1] : ~0ull;
+    }
     __syncthreads();
-    // item (k, q) of this thread: tile index k * kUniqTile + q * kBlock + t (coalesced)
+    // item (k, q) of this thread: tile index k * kUniqTile + q * kBlock + t
+    // (coalesced); pv = the record before it (~0: none).  Past hi the packed
+    // form's values are padding, never flagged (the i < hi tests below).
     auto item = [&](int k, int q, uint64_t& r, uint64_t& pv) {
         const uint32_t x = (uint32_t)(k * kUniqTile + q * kBlock + t);
-        r = s_rec[1 + x];
-        pv = s_rec[x];
+        if (kPacked) {
+            r = unpack(s_raw[x]);
+            pv = x == 0 ? s_prev : unpack(s_raw[x - 1]);
+        } else {
+            r = s_rec[1 + x];
+            pv = s_rec[x];
+        }
     };
     uint64_t C = 0, B = 0;
+    // per sub-tile: this thread's exclusive pair / byte offsets (16-bit fields),
+    // in registers selected by the (uniform) sub-tile index: the loops stay
+    // rolled, so the LDS reads of all sub-tiles are not hoisted together
+    static_assert(kUniqSub == 4, "four register slots");
+    uint64_t exc0 = 0, exc1 = 0, exc2 = 0, exc3 = 0, exb0 = 0, exb1 = 0, exb2 = 0, exb3 = 0;
 #pragma unroll 1
     for (int k = 0; k < kUniqSub; k++) {
         uint64_t c = 0, b = 0;
@@ -1646,8 +1661,15 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
         // 16-bit fields: no carries (a field sums at most kBlock pairs of <= 11 bytes)
         uint64_t ec, eb, tc, tb;
         block_excl_scan2(c, b, ec, eb, tc, tb, lds);
-        s_ex[k][0][t] = ec | (c & 0x0001000100010001ull) << 15;  // the item's own flag rides in bit 15 of its field
-        s_ex[k][1][t] = eb;
+        const uint64_t fc = ec | (c & 0x0001000100010001ull) << 15;  // the item's own flag rides in bit 15 of its field
+        exc0 = k == 0 ? fc : exc0;
+        exc1 = k == 1 ? fc : exc1;
+        exc2 = k == 2 ? fc : exc2;
+        exc3 = k == 3 ? fc : exc3;
+        exb0 = k == 0 ? eb : exb0;
+        exb1 = k == 1 ? eb : exb1;
+        exb2 = k == 2 ? eb : exb2;
+        exb3 = k == 3 ? eb : exb3;
         if (t == 0) {
             s_tot[k][0] = tc;
             s_tot[k][1] = tb;
@@ -1708,7 +1730,9 @@ __global__ __launch_bounds__(kBlock) void k_uniq_sweep(const uint64_t* __restric
     uint64_t rc = s_base[0], rb = s_base[1];
 #pragma unroll 1
     for (int k = 0; k < kUniqSub; k++) {
-        const uint64_t ec = s_ex[k][0][t], eb = s_ex[k][1][t], tc = s_tot[k][0], tb = s_tot[k][1];
+        const uint64_t ec = k == 0 ? exc0 : k == 1 ? exc1 : k == 2 ? exc2 : exc3;
+        const uint64_t eb = k == 0 ? exb0 : k == 1 ? exb1 : k == 2 ? exb2 : exb3;
+        const uint64_t tc = s_tot[k][0], tb = s_tot[k][1];
 #pragma unroll
         for (int q = 0; q < kUniqItems; q++) {
             const uint64_t f = (ec >> (16 * q)) & 0xFFFFull;
