@@ -1527,7 +1527,7 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
 // word's first pair.
 constexpr int kUniqItems = 4;                        // records per thread per tile
 constexpr int kUniqTile = kUniqItems * kBlock;       // item q of thread t: tile base + q * kBlock + t (coalesced)
-static_assert(kUniqItems * 16 <= 64, "per-item prefixes travel as 16-bit fields of one u64");
+static_assert(kUniqItems == 4, "per-item prefixes travel as 8-bit (flags) and 16-bit (bytes) fields");
 
 // digits of v = id0 + 1 <= 2^32 (1..10), branch-free
 __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
@@ -1537,6 +1537,44 @@ __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
 
 __device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
     return (x & 0xFFFFull) + ((x >> 16) & 0xFFFFull) + ((x >> 32) & 0xFFFFull) + (x >> 48);
+}
+
+// 8-bit fields -> 16-bit fields of a u64
+__device__ __forceinline__ uint64_t field8_spread(uint32_t x) {
+    return (uint64_t)(x & 0xFFu) | (uint64_t)((x >> 8) & 0xFFu) << 16 | (uint64_t)((x >> 16) & 0xFFu) << 32 |
+           (uint64_t)(x >> 24) << 48;
+}
+
+// K3's block exclusive scan of a thread's pair flags (c8: one 8-bit field per
+// item, a wave sums at most 64 in a field) and posting bytes (bl / bh: 16-bit
+// fields of items 0-1 / 2-3, at most 64 * 11 per wave): three DPP wave scans
+// (ii_kernels.h wave_incl_scan32) instead of two u64 shuffle scans, then the
+// waves' totals through LDS.  Returns 16-bit fields (no carries: a block field
+// sums at most kBlock * 11) and the block totals.
+__device__ __forceinline__ void uniq_block_scan(uint32_t c8, uint32_t bl, uint32_t bh, uint64_t& ec, uint64_t& eb,
+                                                uint64_t& tc, uint64_t& tb, uint64_t* lds /*2*kWaves*/) {
+    const uint64_t ic = field8_spread(wave_incl_scan32(c8));
+    const uint64_t ib = (uint64_t)wave_incl_scan32(bl) | (uint64_t)wave_incl_scan32(bh) << 32;
+    if (lane_id() == 63) {
+        lds[wave_id()] = ic;
+        lds[kWaves + wave_id()] = ib;
+    }
+    __syncthreads();
+    uint64_t wa = 0, wb = 0;
+    tc = tb = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        const uint64_t sa = lds[w], sb = lds[kWaves + w];
+        if (w < wave_id()) {
+            wa += sa;
+            wb += sb;
+        }
+        tc += sa;
+        tb += sb;
+    }
+    __syncthreads();
+    ec = wa + ic - field8_spread(c8);
+    eb = wb + ib - ((uint64_t)bl | (uint64_t)bh << 32);
 }
 
 // K3 in one pass (decoupled look-back, as k_onesweep): a workgroup takes a
@@ -1558,7 +1596,7 @@ constexpr int kUniqSweepTile = kUniqSub * kUniqTile;  // 4096 records
 // which the dense form leaves to the next word's start and k_post_last.
 static_assert(kSweepTile == 2 * kUniqSweepTile, "K3 tile = half a packed-sort tile");
 template <bool kPacked>
-__global__ __launch_bounds__(kBlock, 8) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
+__global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
                                                        const uint32_t* __restrict__ rec32, uint64_t ncap,
                                                        const uint32_t* __restrict__ btile,
                                                        const uint16_t* __restrict__ tbk,
@@ -1647,21 +1685,22 @@ __global__ __launch_bounds__(kBlock, 8) void k_uniq_sweep(const uint64_t* __rest
     uint64_t exc0 = 0, exc1 = 0, exc2 = 0, exc3 = 0, exb0 = 0, exb1 = 0, exb2 = 0, exb3 = 0;
 #pragma unroll 1
     for (int k = 0; k < kUniqSub; k++) {
-        uint64_t c = 0, b = 0;
+        uint32_t c8 = 0, bl = 0, bh = 0;
 #pragma unroll
         for (int q = 0; q < kUniqItems; q++) {
             uint64_t r, pv;
             item(k, q, r, pv);
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
-                c |= 1ull << (16 * q);
-                b += (uint64_t)(id_digits((r & 0xFFFFFFFFull) + 1) + 1) << (16 * q);
+                c8 |= 1u << (8 * q);
+                const uint32_t d = id_digits((r & 0xFFFFFFFFull) + 1) + 1;
+                if (q < 2) bl += d << (16 * q);
+                else bh += d << (16 * (q - 2));
             }
         }
-        // 16-bit fields: no carries (a field sums at most kBlock pairs of <= 11 bytes)
         uint64_t ec, eb, tc, tb;
-        block_excl_scan2(c, b, ec, eb, tc, tb, lds);
-        const uint64_t fc = ec | (c & 0x0001000100010001ull) << 15;  // the item's own flag rides in bit 15 of its field
+        uniq_block_scan(c8, bl, bh, ec, eb, tc, tb, lds);
+        const uint64_t fc = ec | field8_spread(c8) << 15;  // the item's own flag rides in bit 15 of its field
         exc0 = k == 0 ? fc : exc0;
         exc1 = k == 1 ? fc : exc1;
         exc2 = k == 2 ? fc : exc2;

@@ -70,32 +70,6 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total,
     return wbase + inc - v;
 }
 
-// Exclusive block scan of two values at once (one pair of barriers).
-__device__ __forceinline__ void block_excl_scan2(uint64_t a, uint64_t b, uint64_t& ea, uint64_t& eb, uint64_t& ta,
-                                                 uint64_t& tb, uint64_t* lds /*2*kWaves*/) {
-    const uint64_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
-    if (lane_id() == 63) {
-        lds[wave_id()] = ia;
-        lds[kWaves + wave_id()] = ib;
-    }
-    __syncthreads();
-    uint64_t wa = 0, wb = 0;
-    ta = tb = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-        const uint64_t sa = lds[w], sb = lds[kWaves + w];
-        if (w < wave_id()) {
-            wa += sa;
-            wb += sb;
-        }
-        ta += sa;
-        tb += sb;
-    }
-    __syncthreads();
-    ea = wa + ia - a;
-    eb = wb + ib - b;
-}
-
 // ----------------------------------------------------------------------------
 // Device-wide exclusive scan over n items.  Op provides
 //   uint64_t value(uint64_t i)                 (the item)
@@ -698,7 +672,7 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
 // (launch bound of 4 waves per SIMD: without it the compiler spent 256 VGPRs
 // with spills, one workgroup per CU, 2.4x slower than k_onesweep)
 template <int NT, int IT, int kLbPer = 2>
-__global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,
+__global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,
                                                      uint32_t* __restrict__ kout,
                                                      const uint32_t* __restrict__ btile,
                                                      const uint16_t* __restrict__ tbk,
@@ -746,13 +720,16 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
     const uint32_t h = tbk[tile];
     const uint64_t tile0 = btile[h];
     const uint64_t vend = tile0 * kTileN + (bstart[h + 1] - bstart[h]);
+    // the tile's valid records [0, vrel) in 32-bit tile-relative indices
+    const uint32_t vrel = vend <= tb ? 0u : vend - tb < (uint64_t)kTileN ? (uint32_t)(vend - tb) : (uint32_t)kTileN;
+    const uint32_t wrel = (uint32_t)w * 64 * IT + (uint32_t)l;
 #pragma unroll
     for (int k = 0; k < IT; k++)
-        if (wbase + (uint64_t)k * 64 >= vend) key[k] = ~0u;
+        if (wrel + (uint32_t)k * 64 >= vrel) key[k] = ~0u;
     uint32_t info[IT];  // as k_onesweep: rank in the item's group | group size << 8 | leader lane << 16
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-        const bool valid = wbase + (uint64_t)k * 64 < vend;
+        const bool valid = wrel + (uint32_t)k * 64 < vrel;
         const uint32_t d = (key[k] >> shift) & dmask;
         uint64_t m = __ballot(valid);
 #pragma unroll
@@ -765,17 +742,11 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
         }
         info[k] = valid ? (uint32_t)__popcll(m & lt) | ((uint32_t)__popcll(m) << 8) | ((uint32_t)__builtin_ctzll(m) << 16)
                         : 0xFFFFFFFFu;
+        uint32_t before = 0;
+        if ((info[k] & 0xFFu) == 0u) before = atomicAdd(&s_wcnt[w][d], (info[k] >> 8) & 0xFFu);
+        info[k] = (uint32_t)__shfl((int)before, (int)((info[k] >> 16) & 63u), 64) + (info[k] & 0xFFu);  // -> rank
     }
-    uint32_t before[IT];
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        before[k] = 0;
-        if ((info[k] & 0xFFu) == 0u) before[k] = atomicAdd(&s_wcnt[w][(key[k] >> shift) & dmask], (info[k] >> 8) & 0xFFu);
-    }
-    uint32_t rank[IT];
-#pragma unroll
-    for (int k = 0; k < IT; k++)
-        rank[k] = (uint32_t)__shfl((int)before[k], (int)((info[k] >> 16) & 63u), 64) + (info[k] & 0xFFu);
+    const uint32_t* rank = info;
     __syncthreads();
     uint32_t cw[NW];
     uint32_t tot_d = 0;
@@ -814,7 +785,7 @@ __global__ __launch_bounds__(NT, 4) void k_onesweep_seg(const uint32_t* __restri
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-        if (wbase + (uint64_t)k * 64 < vend) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
+        if (wrel + (uint32_t)k * 64 < vrel) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
     }
     // look-back over the bucket's earlier tiles (k_onesweep's quads of lanes)
     const uint64_t obase = tile0 * kTileN;
