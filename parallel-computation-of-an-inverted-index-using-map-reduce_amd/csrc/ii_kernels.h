@@ -397,19 +397,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
-// Inclusive wave64 scan with DPP (GFX9 row_shr inside the 16-lane rows, then
-// row_bcast:15 / :31 across them): six VALU adds instead of six ds_bpermute
-// round trips.  A lane whose source lies outside its row (or a row that the
-// row mask leaves out) adds the `old` operand, 0.
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return v;
-}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
@@ -1892,7 +1879,7 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
 // places the rest by a wave scan of their byte counts, so the pass reads
 // 8 bytes per posting instead of 16.
 constexpr int kFmtItems = 4;  // groups per wave (2 or 8: slower)
-__global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
+__global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
                                                       const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
                                                       uint8_t* __restrict__ out) {
     constexpr uint64_t kSpan = 64ull * kFmtItems;  // postings of one wave per iteration
@@ -1930,12 +1917,7 @@ __global__ __launch_bounds__(kBlock) void k_fmt_posts(const uint64_t* __restrict
             const uint64_t id = (r[k] & 0xFFFFFFFFull) + 1;
             const uint32_t nd = id_digits(id);
             const uint32_t len = live ? nd + 1u : 0u;
-            uint32_t inc = len;  // inclusive wave scan (64 postings x <= 11 bytes)
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(inc, o, 64);
-                if (lane_id() >= o) inc += t;
-            }
+            const uint32_t inc = wave_incl_scan32(len);  // inclusive wave scan (64 postings x <= 11 bytes)
             if (!live) continue;
             // last posting of the word: the next pair belongs to another word (runs are contiguous)
             const bool last = p + 1 == U || wn[k] != w;

@@ -47,6 +47,19 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
     }
     return v;
 }
+// Inclusive wave64 scan with DPP (GFX9 row_shr inside the 16-lane rows, then
+// row_bcast:15 / :31 across them): six VALU adds instead of six ds_bpermute
+// round trips.  A lane whose source lies outside its row (or a row that the
+// row mask leaves out) adds the `old` operand, 0.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -292,18 +305,18 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
                 tot_d += cw[ww];
             }
         }
-        const uint64_t inc = wave_incl_scan(tot_d);
+        const uint32_t inc = wave_incl_scan32(tot_d);  // (a tile holds at most kTileN keys)
         if (w < kDW && l == 63) s_scan[w] = inc;
         __syncthreads();
-        uint64_t wb = 0, all = 0;
+        uint32_t wb = 0, all = 0;
 #pragma unroll
         for (int ww = 0; ww < kDW; ww++) {
-            const uint64_t sv = s_scan[ww];
+            const uint32_t sv = (uint32_t)s_scan[ww];
             if (ww < w) wb += sv;
             all += sv;
         }
         if (digit_thread) {
-            uint32_t run = (uint32_t)(wb + inc - tot_d);
+            uint32_t run = wb + inc - tot_d;
             s_tstart[t] = run;
 #pragma unroll
             for (int ww = 0; ww < NW; ww++) {
@@ -763,18 +776,18 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
         __hip_atomic_store(status + tile * kRadix + t, ep | (tile == tile0 ? kLbFlagP : kLbFlagA) | tot_d,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint64_t inc = wave_incl_scan(tot_d);
+    const uint32_t inc = wave_incl_scan32(tot_d);  // (a tile holds at most kTileN records)
     if (w < kDW && l == 63) s_scan[w] = inc;
     __syncthreads();
-    uint64_t wb = 0, all = 0;
+    uint32_t wb = 0, all = 0;
 #pragma unroll
     for (int ww = 0; ww < kDW; ww++) {
-        const uint64_t sv = s_scan[ww];
+        const uint32_t sv = (uint32_t)s_scan[ww];
         if (ww < w) wb += sv;
         all += sv;
     }
     if (t < kRadix) {
-        uint32_t run = (uint32_t)(wb + inc - tot_d);
+        uint32_t run = wb + inc - tot_d;
         s_tstart[t] = run;
 #pragma unroll
         for (int ww = 0; ww < NW; ww++) {
