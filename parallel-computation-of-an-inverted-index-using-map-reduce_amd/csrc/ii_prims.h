@@ -761,14 +761,10 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
     }
     const uint32_t* rank = info;
     __syncthreads();
-    uint32_t cw[NW];
-    uint32_t tot_d = 0;
+    uint32_t tot_d = 0;  // (the per-wave counts are read again below: held in registers they spilled)
     if (t < kRadix) {
 #pragma unroll
-        for (int ww = 0; ww < NW; ww++) {
-            cw[ww] = s_wcnt[ww][t];
-            tot_d += cw[ww];
-        }
+        for (int ww = 0; ww < NW; ww++) tot_d += s_wcnt[ww][t];
     }
     const uint64_t ep = epoch << 40;
     if (digit_thread) {
@@ -791,8 +787,9 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
         s_tstart[t] = run;
 #pragma unroll
         for (int ww = 0; ww < NW; ww++) {
+            const uint32_t cnt = s_wcnt[ww][t];
             s_wcnt[ww][t] = run;
-            run += cw[ww];
+            run += cnt;
         }
     }
     __syncthreads();
