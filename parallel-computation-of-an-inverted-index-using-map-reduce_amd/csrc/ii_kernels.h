@@ -1664,12 +1664,12 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             pv = s_rec[x];
         }
     };
-    uint64_t C = 0, B = 0;
-    // per sub-tile: this thread's exclusive pair / byte offsets (16-bit fields),
-    // in registers selected by the (uniform) sub-tile index: the loops stay
-    // rolled, so the LDS reads of all sub-tiles are not hoisted together
+    // 1. every item's flag and posting bytes (per sub-tile: 8-bit flag fields, 16-bit byte
+    //    fields), kept in registers selected by the (uniform) sub-tile index — the loops
+    //    stay rolled, so the LDS reads of all sub-tiles are not hoisted together
     static_assert(kUniqSub == 4, "four register slots");
-    uint64_t exc0 = 0, exc1 = 0, exc2 = 0, exc3 = 0, exb0 = 0, exb1 = 0, exb2 = 0, exb3 = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0, h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    uint32_t tcount = 0, tbytes = 0;  // this thread's pairs / posting bytes
 #pragma unroll 1
     for (int k = 0; k < kUniqSub; k++) {
         uint32_t c8 = 0, bl = 0, bh = 0;
@@ -1683,8 +1683,43 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                 const uint32_t d = id_digits((r & 0xFFFFFFFFull) + 1) + 1;
                 if (q < 2) bl += d << (16 * q);
                 else bh += d << (16 * (q - 2));
+                tcount++;
+                tbytes += d;
             }
         }
+        c0 = k == 0 ? c8 : c0; c1 = k == 1 ? c8 : c1; c2 = k == 2 ? c8 : c2; c3 = k == 3 ? c8 : c3;
+        l0 = k == 0 ? bl : l0; l1 = k == 1 ? bl : l1; l2 = k == 2 ? bl : l2; l3 = k == 3 ? bl : l3;
+        h0 = k == 0 ? bh : h0; h1 = k == 1 ? bh : h1; h2 = k == 2 ? bh : h2; h3 = k == 3 ? bh : h3;
+    }
+    // 2. the tile's totals (one block reduction) and its aggregate published at once, before
+    //    the sub-tile scans: later tiles' look-backs sum it instead of waiting for them
+    {
+        const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tcount), 63);
+        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(tbytes), 63);
+        if (lane_id() == 0) {
+            lds[wave_id()] = wc;
+            lds[kWaves + wave_id()] = wb;
+        }
+    }
+    __syncthreads();
+    uint64_t C = 0, B = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        C += lds[w];
+        B += lds[kWaves + w];
+    }
+    const uint64_t ep = epoch << 40;
+    if (t == 0 || t == 32)
+        __hip_atomic_store(status + 2 * tile + (t >> 5), ep | (tile == 0 ? kLbFlagP : kLbFlagA) | (t == 0 ? C : B),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // (lds is reused by the scans)
+    // 3. per sub-tile: this thread's exclusive pair / byte offsets (16-bit fields)
+    uint64_t exc0 = 0, exc1 = 0, exc2 = 0, exc3 = 0, exb0 = 0, exb1 = 0, exb2 = 0, exb3 = 0;
+#pragma unroll 1
+    for (int k = 0; k < kUniqSub; k++) {
+        const uint32_t c8 = k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3;
+        const uint32_t bl = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
+        const uint32_t bh = k == 0 ? h0 : k == 1 ? h1 : k == 2 ? h2 : h3;
         uint64_t ec, eb, tc, tb;
         uniq_block_scan(c8, bl, bh, ec, eb, tc, tb, lds);
         const uint64_t fc = ec | field8_spread(c8) << 15;  // the item's own flag rides in bit 15 of its field
@@ -1700,8 +1735,6 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             s_tot[k][0] = tc;
             s_tot[k][1] = tb;
         }
-        C += field16_sum(tc);
-        B += field16_sum(tb);
     }
     // look-back, wave 0: lanes 0..31 walk the pair counts, lanes 32..63 the
     // byte counts, each half loading the granules of 32 earlier tiles per
@@ -1709,11 +1742,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
     // rate at which tiles start, so every tile walked far)
     if (t < 64) {
         const uint32_t f = (uint32_t)t >> 5, j = (uint32_t)t & 31u;  // field, distance - 1 of the tile this lane loads
-        const uint64_t v0 = f == 0 ? C : B;
-        const uint64_t ep = epoch << 40;
-        if (j == 0)
-            __hip_atomic_store(status + 2 * tile + f, ep | (tile == 0 ? kLbFlagP : kLbFlagA) | v0, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t v0 = f == 0 ? C : B;  // (the aggregate is published above)
         uint64_t excl = 0;
         bool done = tile == 0;
         for (int64_t base = (int64_t)tile - 1; __ballot(!done) != 0; base -= 32) {
