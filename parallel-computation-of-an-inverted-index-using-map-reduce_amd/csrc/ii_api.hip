@@ -1223,17 +1223,18 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     uint32_t* ov2 = P_<uint32_t>(c->oval2);
     const int dbits = std::max(1, bitlen(c->id_bound));
     uint64_t* pe = P_<uint64_t>(c->pstop);
-    k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, pe, (uint32_t)V, dbits, ok, ov);
+    uint64_t* Pp = P_<uint64_t>(c->P);
+    CK(grow(c->loff, sizeof(uint64_t) * (V + 1)));
+    uint64_t* loff = P_<uint64_t>(c->loff);
+    k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, pe, (uint32_t)V, dbits, ok, ov,
+                                                    P_<uint32_t>(c->llen), Pp, loff);
     CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr));
     c->ord = ov;
     HIPCK(hipEventRecord(c->ev[5], c->st));
 
     // ---- K5: format "word:[ids]\n" lines
-    CK(grow(c->loff, sizeof(uint64_t) * (V + 1)));
     CK(grow(c->letter_off, sizeof(uint64_t) * (II_ALPHABET + 1)));
-    uint64_t* Pp = P_<uint64_t>(c->P);
-    uint64_t* loff = P_<uint64_t>(c->loff);
-    CK(run_scan(c, OpLineOff{ov, P_<uint32_t>(c->llen), ps, pe, Pp, loff}, V, totals + 2));
+    CK(run_scan(c, OpLineOff{ov, loff}, V, totals + 2));
     CK(read_u64(c, totals + 2, &c->out_bytes));
     CK(grow(c->out, std::max<uint64_t>(c->out_bytes, 16)));
     uint8_t* out = P_<uint8_t>(c->out);

@@ -1837,17 +1837,23 @@ __global__ __launch_bounds__(kBlock) void k_wid_post(const uint32_t* __restrict_
 // ---------------------------------------------------------------- K4 order
 // key = letter << dbits | (dmax - df): ascending == (letter, df desc); the
 // stable sort keeps lexicographic order among equal df (main.c:55-64).
+// Also each word's line bytes "word:[" + postings + "\n" -> linelen[j] (by
+// lexid), the value OpLineOff scans in final order: one gather per line
+// there instead of five dependent ones.
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ post_start,
                                                        const uint64_t* __restrict__ post_end,
                                                        uint32_t V, int dbits, uint64_t* __restrict__ okey,
-                                                       uint32_t* __restrict__ oval) {
+                                                       uint32_t* __restrict__ oval, const uint32_t* __restrict__ lex_len,
+                                                       const uint64_t* __restrict__ P, uint64_t* __restrict__ linelen) {
     uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= V) return;
-    uint64_t df = post_end[j] - post_start[j];
+    const uint64_t s = post_start[j], e = post_end[j];
+    uint64_t df = e - s;
     uint64_t dmax = (1ull << dbits) - 1;
     uint64_t letter = (sk[j] >> 59) - 1;
     okey[j] = (letter << dbits) | (dmax - df);
     oval[j] = j;
+    linelen[j] = (uint64_t)lex_len[j] + 3 + (P[e] - P[s]);
 }
 
 // ---------------------------------------------------------------- K5 format
@@ -1864,18 +1870,13 @@ __device__ __forceinline__ void write_word(const uint8_t* __restrict__ text, uin
     }
 }
 
-// line bytes in final order: "word:[" + postings + "\n"
+// line byte offsets in final order: loff[w] holds word w's line bytes
+// (k_order_keys) and receives the line's offset (each item is read and then
+// written by the same thread of k_scan_apply, after k_scan_reduce has read all)
 struct OpLineOff {
     const uint32_t* ord;
-    const uint32_t* lex_len;
-    const uint64_t* post_start;
-    const uint64_t* post_end;
-    const uint64_t* P;
     uint64_t* loff;  // by lexid
-    __device__ uint64_t value(uint64_t i) const {
-        uint32_t w = ord[i];
-        return (uint64_t)lex_len[w] + 3 + (P[post_end[w]] - P[post_start[w]]);
-    }
+    __device__ uint64_t value(uint64_t i) const { return loff[ord[i]]; }
     __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { loff[ord[i]] = ex; }
 };
 
