@@ -1522,10 +1522,6 @@ __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
            (v >= 1000000ull) + (v >= 10000000ull) + (v >= 100000000ull) + (v >= 1000000000ull);
 }
 
-__device__ __forceinline__ uint64_t field16_sum(uint64_t x) {
-    return (x & 0xFFFFull) + ((x >> 16) & 0xFFFFull) + ((x >> 32) & 0xFFFFull) + (x >> 48);
-}
-
 // 8-bit fields -> 16-bit fields of a u64
 __device__ __forceinline__ uint64_t field8_spread(uint32_t x) {
     return (uint64_t)(x & 0xFFu) | (uint64_t)((x >> 8) & 0xFFu) << 16 | (uint64_t)((x >> 16) & 0xFFu) << 32 |
@@ -1535,7 +1531,7 @@ __device__ __forceinline__ uint64_t field8_spread(uint32_t x) {
 // K3's block exclusive scan of a thread's pair flags (c8: one 8-bit field per
 // item, a wave sums at most 64 in a field) and posting bytes (bl / bh: 16-bit
 // fields of items 0-1 / 2-3, at most 64 * 11 per wave): three DPP wave scans
-// (ii_kernels.h wave_incl_scan32) instead of two u64 shuffle scans, then the
+// (ii_prims.h wave_incl_scan32) instead of two u64 shuffle scans, then the
 // waves' totals through LDS.  Returns 16-bit fields (no carries: a block field
 // sums at most kBlock * 11) and the block totals.
 __device__ __forceinline__ void uniq_block_scan(uint32_t c8, uint32_t bl, uint32_t bh, uint64_t& ec, uint64_t& eb,
