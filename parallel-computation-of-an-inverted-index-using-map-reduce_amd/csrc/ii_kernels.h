@@ -815,8 +815,11 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
 // bit 0 = skip the table probe, bit 2 = skip the letter histogram, bit 3 =
 // skip the per-token step (classify, scan and list only), bit 4 = skip the
 // pending tokens (K1c).
+// Launch bound of 8 waves per SIMD: it caps the SGPRs at 78 (52 spilled to
+// VGPR lanes); at the compiler's own 106 SGPRs the SGPR file held 7 waves per
+// SIMD and the pass ran 12.35 ms instead of 11.70 at 10 GB.
 template <int kAblate = 0>
-__global__ __launch_bounds__(kBlock, 6) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
+__global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                      const uint64_t* __restrict__ file_start,
                                                      const uint32_t* __restrict__ file_id,
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
