@@ -5,16 +5,28 @@ Workloads (BASELINE.json configs):
   config3       synthetic Zipf corpus, 10 GB across 10^4 files, vocabulary 10^6,
                 seed 3 — configs[2] on one MI355X; configs[3] ("the same corpus
                 sharded over 2/4/8") for N > 1
-  config5share  configs[4]'s per-GPU share: 12.5 GB across 1.25*10^5 files,
-                vocabulary 10^7, seed 5, one MI355X
+  config5       BASELINE configs[4]: 100 GB across 10^6 files, vocabulary 10^7,
+                seed 5 — the named --gpus 8 run (strong scaling: every rank
+                generates and indexes its ii_partition share); on one GPU only
+                as --rank-share r/N
+  config5share  a configs[4]-sized single-GPU corpus: 12.5 GB across
+                1.25*10^5 files, vocabulary 10^7, seed 5 (ids 0 .. 1.25*10^5)
 A "step" is one full pass of the hot path over the corpus: tokenize (K1), word
 table + lexicographic ids, token sort (K2), unique pairs (K3), final order
 (K4) and the formatted a..z index text (K5), all device-resident — the text
 is already in HBM when the timed region starts; nothing is cached across
 steps (every step re-tokenizes and rebuilds the index from scratch).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config3|config5share]
-                    [--scaling strong|weak]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config3|config5|config5share]
+                    [--scaling strong|weak] [--rank-share r/N] [--letter-split reference|balanced]
+
+--rank-share r/N (one GPU): the share of rank r when the workload is strong-
+scaled over N GPUs — the files ii_partition (M = N, main.c:300-323) gives
+shard r, generated with their GLOBAL ids (for configs[4] at N = 8: 1.25*10^5
+files whose ids span [0, 10^6)); a step maps and reduces that share (the full
+local index, as at N = 1), and an `export` leg times what the rank does before
+the exchange (map + local reduce + ii_export_plan + ii_export).  Verified
+against the oracle's hashes of that share (tests/golden/bench_hashes.json).
 
 --gpus N > 1 without a torch.distributed environment starts
 `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child
@@ -23,8 +35,9 @@ per GPU, RCCL (backend "nccl") for the exchange.  Strong scaling (default):
 the files of the ONE corpus are assigned to ranks by the reference's size
 heuristic (ii_partition with M = N, main.c:300-323); each rank generates only
 its own files, maps and locally reduces them, one all-to-allv routes each
-letter range to its owner (histogram-balanced ranges, SURVEY §8 f4, or the
-reference's 26/N split, main.c:129-130), and the owners merge and format.
+letter range to its owner (by default the reference's reducer split with
+R = N, main.c:129-130, as north_star asks; --letter-split balanced: the
+histogram-balanced ranges of SURVEY §8 f4), and the owners merge and format.
 --scaling weak: every rank indexes its own full-size corpus (seed + 1000*rank).
 
 After the timed loop (outside it) one more step copies the text out and every
@@ -54,8 +67,10 @@ LETTERS = "abcdefghijklmnopqrstuvwxyz"
 WORKLOADS = {
     "config3": dict(bytes=10_000_000_000, files=10_000, vocab=1_000_000, seed=3,
                     label="zipf 10 GB x 10^4 files, vocab 10^6, seed 3"),
+    "config5": dict(bytes=100_000_000_000, files=1_000_000, vocab=10_000_000, seed=5,
+                    label="zipf 100 GB x 10^6 files, vocab 10^7, seed 5 (BASELINE configs[4])"),
     "config5share": dict(bytes=12_500_000_000, files=125_000, vocab=10_000_000, seed=5,
-                         label="zipf 12.5 GB x 1.25*10^5 files, vocab 10^7, seed 5 (configs[4] per-GPU share)"),
+                         label="zipf 12.5 GB x 1.25*10^5 files, vocab 10^7, seed 5 (configs[4]-sized single-GPU corpus)"),
 }
 
 
@@ -79,16 +94,28 @@ def parse():
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--cpu-baseline", choices=["quick", "none"], default="quick")
     p.add_argument("--cpu-slice-kb", type=int, default=25,
-                   help="file size of the reference's 360-file slice (BASELINE.md's protocol: 1000)")
+                   help="file size of the reference's quick 360-file slice (median of 5 per lane)")
+    p.add_argument("--cpu-protocol-kb", type=int, default=1000,
+                   help="file size of BASELINE.md's protocol slice (360 files x 1 MB), one run of the reference at "
+                        "M = cores / R = 26: cpu_baseline.value (0 = skip; minutes per run)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--gen-threads", type=int, default=16)
     p.add_argument("--io-bytes", type=float, default=2e9,
                    help="bytes of the corpus written to files for the file-reader and end-to-end legs (0 = skip)")
-    p.add_argument("--letter-split", choices=["balanced", "reference"], default="balanced",
-                   help="letter ownership of the N>1 exchange: histogram-balanced (SURVEY §8 f4) or the "
-                        "reference's 26/N reducer split (main.c:129-130)")
+    p.add_argument("--letter-split", choices=["balanced", "reference"], default="reference",
+                   help="letter ownership of the N>1 exchange: the reference's 26/N reducer split (main.c:129-130, "
+                        "default) or histogram-balanced ranges (SURVEY §8 f4)")
+    p.add_argument("--rank-share", default=None, metavar="r/N",
+                   help="one GPU: index rank r's ii_partition share of the workload strong-scaled over N GPUs, "
+                        "with its global file ids")
     a = p.parse_args()
+    a.share = None
+    if a.rank_share:
+        r, _, n = a.rank_share.partition("/")
+        a.share = (int(r), int(n))
+        if not (a.share[1] >= 1 and 0 <= a.share[0] < a.share[1]):
+            p.error("--rank-share r/N needs 0 <= r < N")
     if a.no_cpu_baseline:
         a.cpu_baseline = "none"
     w = WORKLOADS[a.workload]
@@ -145,8 +172,25 @@ def pmc_traffic(build):
         return {}, "unreadable %s: %s" % (os.path.basename(files[-1]), e)
     if d.get("bench_line", {}).get("libii_sha16") != build:
         return {}, "%s was measured on another libii.so build" % os.path.basename(files[-1])
-    return ({k: round(v["traffic_bytes_per_launch"]) for k, v in d["kernels"].items()
-             if "traffic_bytes_per_launch" in v}, os.path.basename(files[-1]))
+    return ({k: v for k, v in d["kernels"].items() if "traffic_bytes_per_launch" in v}, os.path.basename(files[-1]))
+
+
+# the kernels of the sort + segmented-reduce phase (K2 token sort + K3), by rocprof name prefix
+PHASE_KERNELS = ("ii::k_sort0_compact", "ii::k_radix_scatter<false, 512, 16, true>", "ii::k_seg_hist",
+                 "ii::k_onesweep", "ii::k_uniq_sweep", "ii::k_radix_scatter<false, 512, 16, false>")
+
+
+def pmc_phase_bytes(traffic):
+    """HBM bytes per step of the phase kernels from the PMC summary (per-launch
+    traffic x launches per step; a step runs k_sort0_compact once)."""
+    steps = traffic.get("ii::k_sort0_compact<true>", {}).get("dispatches_FETCH_SIZE")
+    if not steps:
+        return None
+    tot = 0.0
+    for k, v in traffic.items():
+        if k.startswith(PHASE_KERNELS):
+            tot += v["traffic_bytes_per_launch"] * v["dispatches_FETCH_SIZE"] / steps
+    return tot
 
 
 def safe_mappers(sizes, cores):
@@ -179,15 +223,17 @@ def write_files(text, off, nf, td):
 
 
 def cpu_baseline(a, text, off, runs=5):
-    """CPU baseline, bounded to about a minute by
-    default: the reference itself (oracle/_ref/tema1 = gcc -O2 main.c) on a
-    reference-feasible slice of the same generator — 360 files (its MAX_FILES,
-    main.c:8) of --cpu-slice-kb KB (25; BASELINE.md's protocol slice is 1000,
-    minutes per run) — at M = cores / R = 26 and M = R = cores, median of
-    `runs` each; its as-shipped ASan build (Makefile:2) once for context; and
-    the multithreaded hash-based restatement (oracle ii_oracle_index_mt,
-    bit-exact) over the WHOLE corpus with `cores` threads.
-    value = the better reference median, in the metric's unit."""
+    """CPU baseline: the reference itself
+    (oracle/_ref/tema1 = gcc -O2 main.c) on reference-feasible slices of the
+    same generator — 360 files (its MAX_FILES, main.c:8):
+      protocol_slice  BASELINE.md's slice, 360 x --cpu-protocol-kb (1000) KB, at
+                      M = cores / R = 26, one run (its O(T*V) reducer takes
+                      minutes on a 10^6 vocabulary): `value` when it ran
+      reference_lanes 360 x --cpu-slice-kb (25) KB at M = cores / R = 26 and
+                      M = R = cores, median of `runs` each, and the as-shipped
+                      ASan build (Makefile:2) once for context
+    and the multithreaded hash-based restatement (oracle ii_oracle_index_mt,
+    bit-exact) over the WHOLE corpus with `cores` threads."""
     import ii_ctypes
     cores = host_cores()
     ref = os.path.join(REPO, "oracle", "_ref", "tema1")
@@ -202,9 +248,9 @@ def cpu_baseline(a, text, off, runs=5):
         try:
             write_files(st, so, sl_files, td)
 
-            def timed(binary, M, R):
+            def timed(binary, M, R, wd=td):
                 t0 = time.perf_counter()
-                pr = subprocess.Popen([binary, str(M), str(R), "list.txt"], cwd=td, stdout=subprocess.DEVNULL,
+                pr = subprocess.Popen([binary, str(M), str(R), "list.txt"], cwd=wd, stdout=subprocess.DEVNULL,
                                       stderr=subprocess.DEVNULL)
                 while True:  # a progress line every 30 s (a long slice is not a hang)
                     try:
@@ -236,6 +282,26 @@ def cpu_baseline(a, text, off, runs=5):
         out.update({"value": best["GBps"], "kind": "reference", "M": best["M"], "R": best["R"],
                     "sample": "reference binary on 360 files x %d KB (%.1f MB) of the same generator (vocab %d); "
                               "median of %d" % (a.cpu_slice_kb, sl_bytes / 1e6, a.vocab, runs), "reference_lanes": lanes})
+        if a.cpu_protocol_kb > 0:
+            pb = 360 * 1000 * a.cpu_protocol_kb
+            pt, po = ii_ctypes.zipf_corpus(pb, 360, a.vocab, a.seed + 77, threads=min(8, cores))
+            pm = safe_mappers([int(po[f + 1] - po[f]) for f in range(360)], cores)
+            td = tempfile.mkdtemp(prefix="ii_cpu_")
+            try:
+                write_files(pt, po, 360, td)
+                del pt
+                log("cpu baseline: reference on the protocol slice (360 x %d KB) M=%d R=26, one run"
+                    % (a.cpu_protocol_kb, pm))
+                t = timed(ref, pm, 26, td)
+            finally:
+                shutil.rmtree(td, ignore_errors=True)
+            ps = {"binary": "tema1 (gcc -O2 main.c)", "M": pm, "R": 26, "runs": 1, "seconds": round(t, 2),
+                  "bytes": pb, "GBps": round(pb / t / 1e9, 6)}
+            out["protocol_slice"] = ps
+            out.update({"value": ps["GBps"], "M": pm, "R": 26,
+                        "sample": "reference binary on BASELINE.md's protocol slice: 360 files x %d KB (%.0f MB) of the "
+                                  "same generator (vocab %d), M = %d / R = 26, one run (%.1f s)"
+                                  % (a.cpu_protocol_kb, pb / 1e6, a.vocab, pm, t)})
     # the bit-exact multithreaded restatement at full size
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_py import oracle_index
@@ -250,6 +316,72 @@ def cpu_baseline(a, text, off, runs=5):
     if "value" not in out:  # no reference binary on this host: the restatement is the baseline
         out.update({"value": full["GBps"], "kind": "port", "sample": full["what"]})
     return out
+
+
+def config2_lane(idx, runs=5):
+    """BASELINE configs[1] as-is: the reference's own fixture (test.txt, 355
+    chapter files of 6 novels, 5.76 MB; committed as tests/golden/config2.tar.xz
+    with the reference binary's output), the reference binary (oracle/_ref/tema1)
+    at M = min(cores, 8) / R = 26 — SURVEY's best lane — median of `runs`,
+    beside this GPU's device-resident map + reduce of the same files (median of
+    `runs`), whose output is checked byte for byte against the fixture."""
+    import tarfile
+    import numpy as np
+    import torch
+    cores = host_cores()
+    ref = os.path.join(REPO, "oracle", "_ref", "tema1")
+    td = tempfile.mkdtemp(prefix="ii_c2_")
+    try:
+        with tarfile.open(os.path.join(REPO, "tests", "golden", "config2.tar.xz"), "r:xz") as tar:
+            tar.extractall(td)
+        names = open(os.path.join(td, "list.txt")).read().split()
+        paths = [os.path.join(td, x) for x in names[1:1 + int(names[0])]]
+        expected = {l: open(os.path.join(td, "expected", l + ".txt"), "rb").read() for l in LETTERS}
+        out = {"fixture": "test.txt (355 files, reference fixture)", "cores": cores}
+        sizes = [os.path.getsize(x) for x in paths]
+        B = sum(sizes)
+        out["bytes"] = B
+        if os.path.exists(ref):
+            M = safe_mappers(sizes, min(cores, 8))
+            ts = []
+            for _ in range(runs):  # (the list's paths are relative to td; outputs land in td)
+                t0 = time.perf_counter()
+                subprocess.run([ref, str(M), "26", "list.txt"], cwd=td, check=True, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL)
+                ts.append(time.perf_counter() - t0)
+            out["reference"] = {"binary": "tema1 (gcc -O2 main.c)", "M": M, "R": 26, "runs": runs,
+                                "median_s": round(statistics.median(ts), 4), "all_s": [round(x, 4) for x in ts],
+                                "GBps": round(B / statistics.median(ts) / 1e9, 6)}
+        # the GPU on the same files: text resident in HBM (files back to back, '\n' after each)
+        data = [open(x, "rb").read() for x in paths]
+        buf = bytearray()
+        starts = []
+        for d in data:
+            starts.append(len(buf))
+            buf += d + b"\n"
+        n = len(buf)
+        d_text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        d_text[:n].copy_(torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8)))
+        fs = np.asarray(starts, dtype=np.uint64)
+        ids = np.arange(len(paths), dtype=np.uint32)
+        ts = []
+        for it in range(runs + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            idx.map_device(d_text.data_ptr(), n, fs, ids)
+            idx.reduce(copy_text=False)
+            torch.cuda.synchronize()
+            if it:
+                ts.append(time.perf_counter() - t0)
+        idx.map_device(d_text.data_ptr(), n, fs, ids)
+        idx.reduce(copy_text=True)
+        ok = all(idx.letter_text(i) == expected[l] for i, l in enumerate(LETTERS))
+        out["gpu"] = {"what": "map + reduce, device-resident text, one MI355X", "runs": runs,
+                      "median_ms": round(statistics.median(ts) * 1e3, 3), "GBps": round(B / statistics.median(ts) / 1e9, 4),
+                      "bit_exact_vs_reference": ok}
+        return out
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
 
 
 def io_legs(idx, text, off, io_bytes, cores):
@@ -331,11 +463,24 @@ def main():
     else:
         torch.cuda.set_device(0)
     strong = a.scaling == "strong" or world == 1
+    if a.share and world > 1:
+        sys.exit("bench.py: --rank-share runs one rank's share on one GPU (--gpus 1)")
+    if a.workload == "config5" and world == 1 and not a.share and not a.custom:
+        sys.exit("bench.py: config5 (100 GB) is the 8-GPU workload: --gpus 8, or --rank-share r/8 on one GPU")
 
     # ---- this rank's files, generated on the host, then to HBM
-    log("generating %s (%d rank(s), %s scaling)" % (a.workload, world, "strong" if strong else "weak"))
+    log("generating %s (%d rank(s), %s scaling%s)" % (a.workload, world, "strong" if strong else "weak",
+                                                    ", share %d/%d" % a.share if a.share else ""))
     t0 = time.perf_counter()
-    if strong:
+    if a.share:  # one rank's ii_partition share (main.c:300-323), global ids
+        layout = ii_ctypes.zipf_layout(a.bytes, a.files, a.seed)
+        sizes = [int(x) for x in (layout[1:] - layout[:-1])]
+        order, sb, se = ii_ctypes.partition(sizes, a.share[1])
+        ids = sorted(order[sb[a.share[0]]:se[a.share[0]]])
+        text, off = ii_ctypes.zipf_shard(a.bytes, a.files, a.vocab, a.seed, ids, threads=a.gen_threads)
+        id_bound = a.files
+        total_bytes = int(off[-1])
+    elif strong:
         layout = ii_ctypes.zipf_layout(a.bytes, a.files, a.seed)
         if world > 1:  # the reference's size heuristic, one shard per GPU (main.c:300-323)
             sizes = [int(x) for x in (layout[1:] - layout[:-1])]
@@ -400,6 +545,31 @@ def main():
     ms_per_step = dt / a.steps * 1e3
     value = total_bytes * a.steps / dt / 1e9
 
+    # ---- --rank-share: what the rank does before the exchange (map + local reduce + export), timed apart
+    export_leg = None
+    if a.share:
+        parts = a.share[1]
+        send = None
+        ts = []
+        for it in range(a.warmup + a.steps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            idx.map_device(d_text.data_ptr(), nbytes, file_start, file_ids)
+            idx.reduce_local()
+            sizes = idx.export_plan(parts)
+            soff, stot = ii_dist.prefix(sizes)
+            if send is None or send.numel() < stot:
+                send = torch.empty(max(stot, 8), dtype=torch.uint8, device="cuda")
+            idx.export(parts, send.data_ptr(), soff)
+            torch.cuda.synchronize()
+            if it >= a.warmup:
+                ts.append(time.perf_counter() - t1)
+        est = idx.stats()
+        export_leg = {"what": "map + ii_reduce_local + ii_export_plan + ii_export (%d parts, the reference's "
+                              "reducer letters)" % parts, "ms": round(statistics.median(ts) * 1e3, 3),
+                      "GBps": round(total_bytes / statistics.median(ts) / 1e9, 3), "send_bytes": int(sum(sizes)),
+                      "sort_packed": est.sort_packed, "sort_passes": est.sort_passes}
+
     # ---- outside the timed region: the index itself, against the oracle's hashes
     verified, verify_note, letter_sha = None, None, {}
     if not a.no_verify:
@@ -416,13 +586,14 @@ def main():
             letter_sha = mine
         if rank == 0:
             db = json.load(open(os.path.join(REPO, "tests", "golden", "bench_hashes.json")))["workloads"]
-            exp = db.get(a.workload)
+            key = a.workload + ("/share%dof%d" % a.share if a.share else "")
+            exp = db.get(key)
             if a.custom or not strong or exp is None:
                 verify_note = "no oracle hashes for this corpus (custom size or weak scaling)"
             else:
                 bad = [l for l in LETTERS if letter_sha.get(l) != exp["letters"][l]["sha256"]]
                 verified = not bad and len(letter_sha) == 26
-                verify_note = "26 letters match the oracle (tests/golden/bench_hashes.json)" if verified else \
+                verify_note = "26 letters match the oracle (tests/golden/bench_hashes.json %s)" % key if verified else \
                     "letters differ from the oracle: %s" % "".join(bad)
 
     if rank == 0:
@@ -432,33 +603,45 @@ def main():
         em_ms = sum(emit_ms) / len(emit_ms)
         em_achieved = st.emit_bytes / (em_ms * 1e-3) / 1e9 if em_ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(build)
-        # sort + segmented-reduce phase (K2 token sort + K3 unique), two byte models:
-        #  survey: SURVEY §8d — first pass 8T + 8T_k, each radix pass 16 T_k, the unique
-        #          pass 8 T_k + 8 U + 16 V (what the algorithm must move)
-        #  impl:   what the kernels of this build move — the passes after the first
-        #          as the library counts them (st.sort_bytes: the packed form's u32
-        #          bucket passes move 36 B per kept record against 48 for three u64
-        #          passes), K3 reads the records once (one pass, staged in LDS) and
-        #          writes the pairs, the posting offsets P (every word start and every
-        #          64th pair) and the per-word start / end arrays
+        # sort + segmented-reduce phase (K2 token sort + K3 unique), three byte counts:
+        #  impl (frac, the primary figure): the bytes this build's kernels must move —
+        #          the first pass reads T records (u32 / u64 as K1 wrote them, counted
+        #          as 8 B) and writes the T_k kept ones, the passes after it as the
+        #          library counts them (st.sort_bytes: the packed form's u32 bucket
+        #          passes), K3 reads the sorted records once (u32 in the packed form)
+        #          and writes the pairs, the posting offsets P (every word start and
+        #          every 64th pair) and the per-word start / end arrays
+        #  survey: SURVEY §8d's model with 8-B records — first pass 8T + 8T_k, 16 T_k
+        #          per later pass, the unique pass 8 T_k + 8 U + 16 V — which charges
+        #          the packed passes for u64 records they do not move (secondary)
+        #  pmc:    HBM bytes the counters saw for the phase's kernels (rocprofv3
+        #          FETCH_SIZE x correction + WRITE_SIZE, profiles/*_pmc_traffic.json
+        #          of this very build), when there is such a summary
         T, Tk, U, V = st.tokens, st.sorted_records, st.pairs, st.words
         sp = max(1, st.sort_passes)
         survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
         k3_read = (4 if st.sort_packed else 8) * Tk  # the packed form's K3 reads u32 records
         impl_b = 8 * T + 8 * Tk + st.sort_bytes + k3_read + 8 * U + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
-        ph_gbs = survey_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
+        ph_gbs = impl_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
+        pmc_b = pmc_phase_bytes(traffic) if traffic else None
         cpu = None
         if a.cpu_baseline != "none" and world == 1:
             cpu = cpu_baseline(a, text, off)
+            log("configs[1] lane: the reference and the GPU on test.txt")
+            cpu["config2"] = config2_lane(idx)
         log("file reader and end-to-end legs")
         io, e2e = io_legs(idx, text, off, a.io_bytes, host_cores()) if world == 1 and a.io_bytes > 0 else (None, None)
         wl = WORKLOADS[a.workload]
         workload = "%s: %s" % (a.workload, wl["label"] if not a.custom else "zipf %.4g GB x %d files, vocab %d, seed %d"
                                % (a.bytes / 1e9, a.files, a.vocab, a.seed))
-        if a.workload == "config3":
+        if a.share:
+            workload += "; rank %d's share of %d (ii_partition, global ids)" % a.share
+        elif a.workload == "config3":
             workload += " (BASELINE configs[3]: sharded over %d GPUs by ii_partition)" % world if world > 1 and strong \
                 else " (BASELINE configs[2])" if world == 1 else " per rank (weak scaling)"
+        elif a.workload == "config5" and world > 1 and strong:
+            workload += ", sharded over %d GPUs by ii_partition" % world
         line = {
             "metric": "indexed input GB/s (whole node) + % of HBM peak BW",
             "value": round(value, 3),
@@ -468,7 +651,8 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if strong and world > 1 else "weak",
+            # strong: one corpus whatever N (total work fixed); weak: a corpus per rank
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic Zipf corpus (tools/iigen.c, s~1), device-resident",
@@ -477,25 +661,34 @@ def main():
             "config": {"workload": workload, "bytes": a.bytes if strong else a.bytes * world,
                        "files": a.files if strong else a.files * world, "vocab": a.vocab, "seed": a.seed,
                        "bytes_rank0": nbytes, "files_rank0": len(ids),
+                       "rank_share": "%d/%d" % a.share if a.share else None,
                        "parallelism": "files by size over %d GPU(s) + letter-range all-to-allv" % world
                        if world > 1 else "one GPU",
-                       "letter_split": a.letter_split if world > 1 else None},
+                       "letter_split": a.letter_split if world > 1 or a.share else None},
             # dominant kernel: the tokenizer (K1b); algorithmic bytes = B + 8*T per launch
             "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
                          "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(em_achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic.get("ii::k_tok_emit<0>"), "traffic_source": traffic_src,
+                         "traffic": round(traffic["ii::k_tok_emit"]["traffic_bytes_per_launch"])
+                         if "ii::k_tok_emit" in traffic else None,
+                         "traffic_raw": round(traffic["ii::k_tok_emit"]["traffic_raw_bytes_per_launch"])
+                         if "traffic_raw_bytes_per_launch" in traffic.get("ii::k_tok_emit", {}) else None,
+                         "traffic_source": traffic_src,
                          "bytes_per_launch": st.emit_bytes, "ms_per_launch": round(em_ms, 4)},
             "roofline_sort": {"bound": "hbm", "kernel": "k_radix_scatter (token sort passes)",
                               "achieved": round(sc_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(sc_achieved / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
             "roofline_sort_phase": {"bound": "hbm", "phase": "token sort + segmented unique (K2 + K3)",
-                                    "model": "SURVEY §8d", "achieved": round(ph_gbs, 1), "peak": HBM_PEAK_GBS,
+                                    "model": "bytes this build's kernels must move (impl)",
+                                    "achieved": round(ph_gbs, 1), "peak": HBM_PEAK_GBS,
                                     "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 4),
-                                    "bytes_per_step": survey_b, "impl_bytes_per_step": impl_b,
-                                    "impl_frac": round(impl_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                    "bytes_per_step": impl_b, "survey_bytes_per_step": survey_b,
+                                    "survey_frac": round(survey_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                     if ph_ms > 0 else 0.0,
+                                    "pmc_bytes_per_step": round(pmc_b) if pmc_b else None,
+                                    "pmc_frac": round(pmc_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                    if pmc_b and ph_ms > 0 else None,
                                     "ms_per_step": round(ph_ms, 4),
                                     "first_pass": {"kernel": "k_sort0_compact", "ms": round(st.sort0_ms, 4),
                                                    "bytes": st.sort0_bytes,
@@ -509,7 +702,9 @@ def main():
                            "emit_ms", "resolve_ms"]},
             "counts": {"tokens": st.tokens, "pairs": st.pairs, "words": st.words, "long_tokens": st.long_tokens,
                        "out_bytes": st.out_bytes, "sort_passes": st.sort_passes, "table_cap": st.table_cap,
-                       "resolved_tokens": st.resolved_tokens, "sorted_records": st.sorted_records},
+                       "resolved_tokens": st.resolved_tokens, "sorted_records": st.sorted_records,
+                       "sort_packed": st.sort_packed, "files": len(ids)},
+            "export": export_leg,
             "output_letter_sha256": letter_sha if letter_sha else None,
             "libii_sha16": build,
             "gen_seconds": round(gen_s, 2),

@@ -170,7 +170,7 @@ static uint32_t or_digits(uint32_t v) {
 
 /* Format one letter's entries (writer, main.c:227-234). Returns malloc'd text. */
 static char *or_reduce_letter(or_dict *d, uint64_t *out_len) {
-    qsort(d->e, d->n, sizeof(or_entry), or_cmp);
+    if (d->n) qsort(d->e, d->n, sizeof(or_entry), or_cmp); /* (qsort of a null array is UB, even of 0 items: UBSan) */
     uint64_t total = 0;
     for (uint32_t i = 0; i < d->n; i++) {
         total += d->e[i].len + 4; /* ":[" "]\n" */
@@ -456,6 +456,8 @@ int main(int argc, char **argv) {
         if (fscanf(fl, "%4095s", names[i]) != 1) {
             fprintf(stderr, "Error reading file name from input file list\n");
             fclose(fl);
+            for (int k = 0; k <= i; k++) free(names[k]);
+            free(names);
             return -1;
         }
     }
@@ -481,17 +483,23 @@ int main(int argc, char **argv) {
     char *out;
     uint64_t loff[OR_ALPHA + 1];
     ii_oracle_index(text ? text : (unsigned char *)"", off, ids, (uint32_t)count, &out, loff);
+    int rc = 0;
     if (num_reducers > 0) {
-        for (int l = 0; l < OR_ALPHA; l++) {
+        for (int l = 0; l < OR_ALPHA && rc == 0; l++) {
             char fn[16];
             snprintf(fn, sizeof(fn), "%c.txt", 'a' + l);
             FILE *o = fopen(fn, "w");
-            if (!o) { fprintf(stderr, "Error creating output file: %s\n", fn); return -1; }
+            if (!o) { fprintf(stderr, "Error creating output file: %s\n", fn); rc = -1; break; }
             fwrite(out + loff[l], 1, loff[l + 1] - loff[l], o);
             fclose(o);
         }
     }
-    free(out);
-    return 0;
+    ii_oracle_free(out);
+    for (int i = 0; i < count; i++) free(names[i]);
+    free(names);
+    free(text);
+    free(off);
+    free(ids);
+    return rc;
 }
 #endif

@@ -41,7 +41,8 @@ struct ii_ctx {
     const uint8_t* text = nullptr;
     uint64_t nbytes = 0;
     uint32_t nfiles = 0;
-    uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df and the id sort bits)
+    uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df)
+    bool fid_ident = true;  // the mapped files' id0s are 0, 1, 2, ... (K1's shard-local file index == id0)
     DBuf fstart, fid;
     std::vector<uint64_t> h_fstart;  // host copies of the mapped files' starts / ids
     std::vector<uint32_t> h_fid;
@@ -84,6 +85,7 @@ struct ii_ctx {
     int part_lo[II_MAX_PARTS] = {0}, part_hi[II_MAX_PARTS] = {0};  // letter range of every export part
 
     uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
+    bool test_lb_timeout = false;  // test knob II_TEST_LB_TIMEOUT: K3's timeout flag raised (its check must fail)
     uint32_t retries = 0;
     bool mapped = false, have_pairs = false, reduced = false;
     uint64_t* rec_sorted = nullptr;
@@ -375,6 +377,9 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     return II_OK;
 }
 
+// *p |= bits (one thread; the II_TEST_LB_TIMEOUT test knob)
+__global__ void k_set_bits(uint64_t* p, unsigned long long bits) { atomicOr((unsigned long long*)p, bits); }
+
 // Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
 // W-bit key when the other W - m key bits and the F id bits fit a u32 and
 // leave two LSD passes of <= kRadixBits bits; 0 = not packable.
@@ -388,9 +393,10 @@ static int packed_top_bits(int W, int F) {
 // The token sort of local_reduce in the packed form: k_sort0_compact (dedup,
 // key remap, compaction, counts of the top digit per workgroup) into *k2, the
 // MSD scatter into buckets of u32 records (*k, padded), per-bucket digit
-// counts, two bucket-local onesweep passes (*k -> *k2 -> *k, the last one
-// writing the dense u64 records).  Keys sit at bits [lo, lo + W) of the
-// records, ids below 2^F.  On return *k holds the *n_out sorted records.
+// counts, two bucket-local onesweep passes (*k -> *k2 -> *k, both writing u32
+// records in the padded buckets; K3 reads that layout).  Keys sit at bits
+// [lo, lo + W) of the records, ids below 2^F.  On return *k holds the *n_out
+// sorted records.
 static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F, int m,
                            const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
     *passes = 0;
@@ -489,8 +495,9 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
 
 // K3: distinct (lexid, id0) pairs of the sorted records r[0, n), their
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
-// (post_start[V] = U).  Sets c->U.
-static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed) {
+// (post_start[V] = U).  Sets c->U.  fmap: id0 of every shard-local file index
+// the records carry (null: the records carry id0s).
+static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed, const uint32_t* fmap) {
     c->xpairs = false;
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
@@ -524,19 +531,27 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-            P_<unsigned long long>(c->counters) + C_OVERFLOW);
+            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
         k_uniq_sweep<false><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
-            P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW);
+            P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW,
+            fmap);
         k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     }
     if (wid)
         k_wid_post<<<grid_for(c->V), kBlock, 0, c->st>>>(P_<uint32_t>(c->widl), (uint32_t)c->V, ps_k, pe_k, ps, pe);
     HIPCK(hipGetLastError());
+    // K3's look-back flags kLbTimeout instead of hanging (a predecessor tile that never
+    // published reads as a prefix of 0): the pairs and offsets are then wrong — an error
+    uint64_t* ovf = P_<uint64_t>(c->counters) + C_OVERFLOW;
+    if (c->test_lb_timeout) k_set_bits<<<1, 1, 0, c->st>>>(ovf, kLbTimeout);
+    uint64_t flags = 0;
+    HIPCK(hipMemcpyAsync(&flags, ovf, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
     CK(read_u64(c, ps + c->V, &c->U));
+    if (flags & kLbTimeout) return II_ERR_INTERNAL;
     HIPCK(hipMemcpyAsync(Pp + c->U, totals + 6, sizeof(uint64_t), hipMemcpyDeviceToDevice, c->st));
     return II_OK;
 }
@@ -565,6 +580,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
         ii_close(c);
         return II_ERR_NOMEM;
     }
+    c->test_lb_timeout = getenv("II_TEST_LB_TIMEOUT") && !strcmp(getenv("II_TEST_LB_TIMEOUT"), "1");
     const char* s = getenv("II_TABLE_LOG2");
     if (s && atoi(s) >= 10 && atoi(s) <= 30) c->big_cap = 1ull << atoi(s);
     memset(&c->stats, 0, sizeof(c->stats));
@@ -678,7 +694,6 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     CK(grow(c->chunk_hist, sizeof(uint32_t) * 26 * nch));
     uint64_t* chunk_cnt = P_<uint64_t>(c->chunk_cnt);
     const uint64_t* fstart = P_<uint64_t>(c->fstart);
-    const uint32_t* fid = P_<uint32_t>(c->fid);
 
     // the separator contract, checked on the device (totals[9]); the host looks once, with the map's
     // other results
@@ -704,7 +719,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     }
     CK(grow(c->pend_cnt, sizeof(uint32_t) * nch));
     CK(grow(c->chunk_files, sizeof(uint32_t) * 3 * nch));
-    k_chunk_files<<<grid_for(nch), kBlock, 0, c->st>>>(fstart, fid, c->nfiles, c->nbytes, kChunk, nch,
+    k_chunk_files<<<grid_for(nch), kBlock, 0, c->st>>>(fstart, c->nfiles, c->nbytes, kChunk, nch,
                                                       P_<uint32_t>(c->chunk_files));
     const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;  // the long queue grows on overflow
     if (c->long_cap < std::max<uint64_t>(1 << 16, t_est / 64)) c->long_cap = std::max<uint64_t>(1 << 16, t_est / 64);
@@ -723,7 +738,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
-        k_tok_emit<0><<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, fid, chunk_cnt,
+        k_tok_emit<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, chunk_cnt,
                                                        c->rec_cap, tab,
                                                        P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
                                                        P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
@@ -795,6 +810,7 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
     }
     c->nfiles = nfiles;
     c->id_bound = nfiles ? file_id0[nfiles - 1] + 1 : 0;
+    c->fid_ident = !nfiles || file_id0[nfiles - 1] == nfiles - 1;  // ascending ids: the last is nfiles - 1 iff all are i
     c->h_fstart.assign(file_start, file_start + nfiles);
     c->h_fid.assign(file_id0, file_id0 + nfiles);
     c->part_valid = false;
@@ -1169,7 +1185,8 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     uint64_t* r2 = P_<uint64_t>(c->rec2);
     const int lb = std::max(1, bitlen((wid ? c->NW : V) - 1));
     uint64_t Tk = T;
-    const int F = std::max(1, bitlen(c->id_bound ? c->id_bound - 1 : 0));
+    // the records carry shard-local file indices (k_chunk_files): F bits for this map's files
+    const int F = std::max(1, bitlen(c->nfiles ? c->nfiles - 1 : 0));
     c->sort_packed = false;
     const int m = packed_top_bits(lb, F);
     if (m)
@@ -1188,7 +1205,7 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     }
 
     // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
-    CK(run_unique(c, r, Tk, wid, c->sort_packed));
+    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_ident ? nullptr : P_<uint32_t>(c->fid)));
     c->wid_pairs = wid;
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;
@@ -1506,7 +1523,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
-    CK(run_unique(c, r, NP, false, false));  // the owner's merged pairs: dense u64 records
+    CK(run_unique(c, r, NP, false, false, nullptr));  // the owner's merged pairs: dense u64 records of id0s
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)(p1 + p2);
     c->have_pairs = true;

@@ -231,12 +231,18 @@ __device__ __forceinline__ uint32_t file_of(const uint64_t* __restrict__ start, 
     return f_lo;
 }
 
-// Per K1 chunk c: {first file, last file, id0 of the first file} — one
-// binary search per chunk for the whole grid, instead of a serial search by
-// one thread at the start of every K1b / K1c workgroup (~28 dependent loads
-// in each workgroup's critical path).
-__global__ __launch_bounds__(kBlock) void k_chunk_files(const uint64_t* __restrict__ file_start,
-                                                        const uint32_t* __restrict__ file_id, uint32_t nfiles,
+// Per K1 chunk c: {first file, last file, first file again} — one binary
+// search per chunk for the whole grid, instead of a serial search by one
+// thread at the start of every K1b / K1c workgroup (~28 dependent loads in
+// each workgroup's critical path).
+// File numbers in the K1 records are SHARD-LOCAL: the index of the file in the
+// mapped file table (0 .. nfiles - 1), dense and, since files are mapped in
+// ascending id0 order, monotone in id0.  The id bits of the token sort then
+// depend on the shard's file count, not on the global list (a rank of an
+// ii_partition share whose ids span [0, 10^6) sorts 17-bit indices, not 20-bit
+// ids); K3 maps an index back to its id0 (k_uniq_sweep, fmap) when it writes
+// the pairs.
+__global__ __launch_bounds__(kBlock) void k_chunk_files(const uint64_t* __restrict__ file_start, uint32_t nfiles,
                                                         uint64_t nbytes, uint64_t chunk, uint64_t nch,
                                                         uint32_t* __restrict__ cf) {
     const uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_files(const uint64_t* __restri
     const uint32_t f1 = file_of(file_start, f0, nfiles - 1, hi - 1);
     cf[3 * c] = f0;
     cf[3 * c + 1] = f1;
-    cf[3 * c + 2] = file_id[f0];
+    cf[3 * c + 2] = f0;
 }
 
 // The 16 bytes at g, a multiple of 16 (the text is 16-byte aligned); bytes
@@ -759,9 +765,8 @@ __device__ __forceinline__ TokKey general_key(const uint8_t* __restrict__ text, 
 // than 12 letters (hashed keys) are queued for k_long_verify.
 template <bool kSlow>
 __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t c,
-                                                const uint64_t* __restrict__ file_start,
-                                                const uint32_t* __restrict__ file_id, uint32_t f_lo, uint32_t f_hi,
-                                                uint32_t fid0, uint64_t cbase, uint32_t wrap, uint32_t rot,
+                                                const uint64_t* __restrict__ file_start, uint32_t f_lo, uint32_t f_hi,
+                                                uint64_t cbase, uint32_t wrap, uint32_t rot,
                                                 bool narrow, uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
                                                 const Table& tab, uint64_t* __restrict__ rec, uint32_t* hist,
                                                 LongTok* __restrict__ longs, uint64_t long_per) {
@@ -788,7 +793,7 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
             if (narrow) {
                 reinterpret_cast<uint32_t*>(rec + cbase)[jr] = (uint32_t)slot;
             } else {
-                const uint32_t f = f_lo == f_hi ? fid0 : file_id[file_of(file_start, f_lo, f_hi, pos)];
+                const uint32_t f = f_lo == f_hi ? f_lo : file_of(file_start, f_lo, f_hi, pos);
                 rec[cbase + jr] = (slot << 32) | f;
             }
         }
@@ -811,23 +816,39 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
     }
 }
 
-// kAblate (timing experiments only, tools/k1_ablate.hip; the product uses 0):
-// bit 0 = skip the table probe, bit 2 = skip the letter histogram, bit 3 =
-// skip the per-token step (classify, scan and list only), bit 4 = skip the
-// pending tokens (K1c).
-// Launch bound of 8 waves per SIMD: it caps the SGPRs at 78 (52 spilled to
-// VGPR lanes); at the compiler's own 106 SGPRs the SGPR file held 7 waves per
-// SIMD and the pass ran 12.35 ms instead of 11.70 at 10 GB.
-template <int kAblate = 0>
-__global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
-                                                     const uint64_t* __restrict__ file_start,
-                                                     const uint32_t* __restrict__ file_id,
-                                                     uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
-                                                     uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
-                                                     uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
-                                                     const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
-                                                     uint64_t long_per, uint32_t narrow_keys) {
-    __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
+// The fast path's hot-table probe (K1b step 3): the slot of a token's word
+// from the two 16-B slot pairs that begin its probe order, kSlotNone when the
+// word is left to K1c.  The home slot's pair first; only a lane whose home pair
+// is full without its key loads the next pair: the vector L1 handles a probe
+// lane by lane (random lines), so the lanes left out of an instruction are
+// what it saves.  (A policy type: tools/k1_ablate.hip times the same kernel
+// body with other probes, e.g. none.)
+struct HotProbe {
+    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
+                                                   uint64_t pos) const {
+        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
+        ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
+        if (fast) qa = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
+        uint32_t match = (uint32_t)(qa.x == key) | ((uint32_t)(qa.y == key) << 1);
+        uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
+        if (fast && !(match | empty)) {
+            qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
+            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
+            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
+        }
+        return fast ? bucket_resolve(t, match, empty, key, bbase, start, pos) : kSlotNone;
+    }
+};
+
+// K1b for the chunk of this wave (the kernel body; Probe: HotProbe in the product).
+template <class Probe>
+__device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
+                                               const uint64_t* __restrict__ file_start,
+                                               uint64_t* __restrict__ chunk_off, uint64_t cap, const Table& tab,
+                                               uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
+                                               uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
+                                               const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
+                                               uint64_t long_per, uint32_t narrow_keys, EmitLds* s_lds) {
     const uint64_t c = wave_chunk();
     if (c >= nch) return;
     EmitLds& W = s_lds[c - (uint64_t)blockIdx.x * kWG];
@@ -835,7 +856,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
     const uint64_t chunk_lo = c * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
     // the chunk's files (k_chunk_files), wave-uniform
-    const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1], fid0 = cf[3 * c + 2];
+    const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1];
     const bool fsame = f_lo == f_hi;
     const bool narrow = chunk_narrow(cap, cf, c);
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
@@ -885,10 +906,6 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
             for (uint32_t m = kept[1]; m; m &= m - 1) W.off[o++] = (uint16_t)(16 * (64 + l) + __builtin_ctz(m));
         }
         wave_sync();
-        if (kAblate & 8) {  // rounds without the per-token step
-            out += ntok;
-            continue;
-        }
         const uint32_t pbase = (uint32_t)(lo - chunk_lo);
         // 3. keys + cooperative hot-bucket probes, one token per lane (issuing
         //    the next batch's probes before resolving this one measured slower:
@@ -899,32 +916,13 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
             const uint32_t p = valid ? W.off[q] : 0u;
             TokKey tk{0ull, 0u, 0u};
             const bool fast = valid && round_fast_key(W.text, W.mask, p, tk);
-            const uint32_t home = hot_slot(tk.key, tab.seed);
-            if (!(kAblate & 4) && fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS: same-letter lanes serialize in the LDS unit, not in VALU
-            uint32_t slot = kSlotNone;
-            if (kAblate & 1) {
-                if (fast) slot = home;
-            } else {
-                // the home slot's pair (16 B) first; only a lane whose home pair is full without its key
-                // loads the next pair: the vector L1 handles a probe lane by lane (random lines), so the
-                // lanes left out of an instruction are what it saves
-                const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
-                ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
-                if (fast) qa = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + start);
-                uint32_t match = (uint32_t)(qa.x == tk.key) | ((uint32_t)(qa.y == tk.key) << 1);
-                uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
-                if (fast && !(match | empty)) {
-                    qb = *reinterpret_cast<const ulonglong2*>(tab.keys + bbase + ((start + 2) & (kBucket - 2)));
-                    match |= ((uint32_t)(qb.x == tk.key) << 2) | ((uint32_t)(qb.y == tk.key) << 3);
-                    empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
-                }
-                if (fast) slot = bucket_resolve(tab, match, empty, tk.key, bbase, start, lo + p);
-            }
+            if (fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS: same-letter lanes serialize in the LDS unit, not in VALU
+            const uint32_t slot = Probe()(tab, fast, tk.key, hot_slot(tk.key, tab.seed), lo + p);
             const bool resolved = fast && slot != kSlotNone;
             bool pf = fast && !resolved, ps = valid && !fast;
             uint64_t mf = __ballot(pf);
             if (narrow && npf + (uint32_t)__popcll(mf) > narrow_keys) {  // (wave-uniform, adversarial) no room for
-                if (!(kAblate & 4) && pf) atomicSub(&W.hist[tk.first], 1u);  // more keys: K1c re-reads them from the
+                if (pf) atomicSub(&W.hist[tk.first], 1u);                     // more keys: K1c re-reads them from the
                 ps = ps || pf;                                                // text (and counts their letters)
                 pf = false;
                 mf = 0;
@@ -934,7 +932,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
                 if (narrow) {
                     rec32[jr] = slot;
                 } else {
-                    const uint32_t f = fsame ? fid0 : file_id[file_of(file_start, f_lo, f_hi, lo + p)];
+                    const uint32_t f = fsame ? f_lo : file_of(file_start, f_lo, f_hi, lo + p);
                     rec[cbase + jr] = ((uint64_t)slot << 32) | f;
                 }
             } else if (pf) {
@@ -955,18 +953,31 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
     //    of this wave stored: the stores are complete (vmcnt) before the loads.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (!(kAblate & 16)) {
-        resolve_pending<false>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, narrow, pend_end, pend,
-                               npf, tab, rec, W.hist, longs, long_per);
-        resolve_pending<true>(text, nbytes, c, file_start, file_id, f_lo, f_hi, fid0, cbase, wrap, rot, narrow, pend_end, pend,
-                              nps, tab, rec, W.hist, longs, long_per);
-    }
+    resolve_pending<false>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, pend_end, pend, npf, tab,
+                           rec, W.hist, longs, long_per);
+    resolve_pending<true>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, pend_end, pend, nps, tab,
+                          rec, W.hist, longs, long_per);
     wave_sync();
     if (l < 26) chunk_hist[c * 26 + l] = W.hist[l];
     if (l == 0) {
         pend_cnt[c] = npf | (nps << 16);
         if (cap) chunk_off[c] = out;  // fixed-capacity layout: the chunk's token count
     }
+}
+
+// K1b.  Launch bound of 8 waves per SIMD: it caps the SGPRs at 78 (52 spilled
+// to VGPR lanes); at the compiler's own 106 SGPRs the SGPR file held 7 waves
+// per SIMD and the pass ran 12.35 ms instead of 11.70 at 10 GB.
+__global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
+                                                     const uint64_t* __restrict__ file_start,
+                                                     uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
+                                                     uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
+                                                     uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
+                                                     const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
+                                                     uint64_t long_per, uint32_t narrow_keys) {
+    __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
+    tok_emit_chunk<HotProbe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
+                             longs, long_per, narrow_keys, s_lds);
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
@@ -1305,7 +1316,7 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 
 // ---------------------------------------------------------------- K2 first pass
 // First pass of the token sort over the records in text order
-// (slot << 32 | file id0), one workgroup per contiguous range, tiles of
+// (slot << 32 | shard-local file index), one workgroup per contiguous range, tiles of
 // kCTile records with the scatter's item mapping:
 //  * drops repeated (hot word, file) records: a record whose slot is a
 //    hot-table slot and whose file is the tile's epoch file is dropped when
@@ -1507,7 +1518,7 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
 }
 
 // ---------------------------------------------------------------- K3 unique + posting bytes
-// Records sorted by (lexid, id0): the first of each equal run is a distinct
+// Records sorted by (lexid, file): the first of each equal run is a distinct
 // (word, file) pair (main.c:176-184, add_number main.c:67-77); its posting
 // "id0+1" takes its digits + 1 bytes (the following ' ' or ']',
 // main.c:228-234).  One reduce-then-scan yields both prefixes: uniq[u] = the
@@ -1518,6 +1529,11 @@ __global__ __launch_bounds__(kBlock) void k_remap(uint64_t* __restrict__ rec, ui
 constexpr int kUniqItems = 4;                        // records per thread per tile
 constexpr int kUniqTile = kUniqItems * kBlock;       // item q of thread t: tile base + q * kBlock + t (coalesced)
 static_assert(kUniqItems == 4, "per-item prefixes travel as 8-bit (flags) and 16-bit (bytes) fields");
+
+// id0 of a record's file: the records of a map carry shard-local file indices
+// (k_chunk_files); fmap = the mapped files' id0s, or null when index == id0
+// (the file table is 0, 1, 2, ...; the owners' merged pairs carry id0s)
+__device__ __forceinline__ uint32_t file_id0(const uint32_t* __restrict__ fmap, uint32_t f) { return fmap ? fmap[f] : f; }
 
 // digits of v = id0 + 1 <= 2^32 (1..10), branch-free
 __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
@@ -1591,7 +1607,8 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                                                        uint64_t* __restrict__ post_start, uint64_t* __restrict__ post_end,
                                                        uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
-                                                       uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err) {
+                                                       uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err,
+                                                       const uint32_t* __restrict__ fmap) {
     // the tile staged in LDS (scanned, then written after the look-back): u64
     // records from [1] with the record before the tile at [0], or in the packed
     // form the raw u32 records (16 KiB, 8 workgroups per CU instead of 3) and
@@ -1679,7 +1696,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
                 c8 |= 1u << (8 * q);
-                const uint32_t d = id_digits((r & 0xFFFFFFFFull) + 1) + 1;
+                const uint32_t d = id_digits((uint64_t)file_id0(fmap, (uint32_t)r) + 1) + 1;
                 if (q < 2) bl += d << (16 * q);
                 else bh += d << (16 * (q - 2));
                 tcount++;
@@ -1796,7 +1813,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                 item(k, q, r, pv);
                 const uint64_t uu = rc + (f & 0x7FFFull);
                 const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
-                uniq[uu] = r;
+                uniq[uu] = (r & ~0xFFFFFFFFull) | file_id0(fmap, (uint32_t)r);
                 const bool wstart = pv == ~0ull || key != pkey;
                 // P is read at word starts (k_fmt_words, OpLineOff) and at the
                 // first posting of every 64 (k_fmt_posts) only

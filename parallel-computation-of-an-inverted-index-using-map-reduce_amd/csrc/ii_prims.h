@@ -682,7 +682,7 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
 // records [btile[h] * tile, + count of h) are valid; the look-back stops at
 // the bucket's first tile, which publishes an inclusive prefix at once.
 // Digit d of bucket h starts at the bucket's padded start + dbase[h * dstride + d].
-// (launch bound of 4 waves per SIMD: without it the compiler spent 256 VGPRs
+// (launch bound of 6 waves per SIMD: without one the compiler spent 256 VGPRs
 // with spills, one workgroup per CU, 2.4x slower than k_onesweep)
 template <int NT, int IT, int kLbPer = 2>
 __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,

@@ -201,8 +201,9 @@ static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count
 }
 
 /* Second half: letter owners, export, exchange, merge, order + format.
- * owner[l] receives the context holding letter l. */
-static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
+ * owner[l] receives the context holding letter l.  The exchange buffers are
+ * freed by the caller (multi_exchange), on every return. */
+static int multi_exchange_body(int G, shard *sh, ii_ctx **owner) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
     const int distinct = ndev >= G;
@@ -250,10 +251,15 @@ static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
         pthread_join(th[g], NULL);
         if (sh[g].rc != II_OK && rc == II_OK) rc = sh[g].rc;
     }
+    return rc;
+}
+
+static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
+    const int rc = multi_exchange_body(G, sh, owner);
     for (int g = 0; g < G; g++) {
         (void)hipSetDevice(sh[g].dev);
-        (void)hipFree(sh[g].d_send);
-        (void)hipFree(sh[g].d_recv);
+        if (sh[g].d_send) (void)hipFree(sh[g].d_send);
+        if (sh[g].d_recv) (void)hipFree(sh[g].d_recv);
         sh[g].d_send = sh[g].d_recv = NULL;
     }
     return rc;
@@ -302,6 +308,26 @@ static int write_partials(shard *sh, int G, ii_ctx *single, const uint32_t *emit
     return rc;
 }
 
+/* Everything main() allocates, released on every return path (the ASan/UBSan
+ * build of tests/test_sanitizers.py runs the list-parsing errors too). */
+typedef struct {
+    ii_file *files;
+    uint64_t *sizes;
+    char **names;
+    int nnames;
+    uint32_t *order, *sb, *se;
+} cli_state;
+
+static void cli_free(cli_state *c) {
+    for (int i = 0; i < c->nnames; i++) free(c->names[i]);
+    free(c->names);
+    free(c->files);
+    free(c->sizes);
+    free(c->order);
+    free(c->sb);
+    free(c->se);
+}
+
 int main(int argc, char **argv) {
     if (argc < 4) {
         fprintf(stderr, "Usage: %s <num_mappers> <num_reducers> <input_file_list>\n", argv[0]); /* main.c:249 */
@@ -322,33 +348,52 @@ int main(int argc, char **argv) {
         return -1;
     }
     if (count < 0) count = 0;
-    ii_file *files = calloc((size_t)count + 1, sizeof(ii_file));
-    uint64_t *sizes = calloc((size_t)count + 1, sizeof(uint64_t));
-    char **names = calloc((size_t)count + 1, sizeof(char *));
+    /* any number of files (the reference overflows files[MAX_FILES] past 360, main.c:8, 270) */
+    cli_state cs = {0};
+    cs.files = calloc((size_t)count + 1, sizeof(ii_file));
+    cs.sizes = calloc((size_t)count + 1, sizeof(uint64_t));
+    cs.names = calloc((size_t)count + 1, sizeof(char *));
+    if (!cs.files || !cs.sizes || !cs.names) {
+        fprintf(stderr, "Memory allocation failed for file name\n");
+        fclose(fl);
+        cli_free(&cs);
+        return -1;
+    }
+    ii_file *files = cs.files;
+    uint64_t *sizes = cs.sizes;
     for (int i = 0; i < count; i++) {
-        names[i] = malloc(4096);
-        if (!names[i]) {
+        cs.names[i] = malloc(4096);
+        if (!cs.names[i]) {
             fprintf(stderr, "Memory allocation failed for file name\n");
             fclose(fl);
+            cli_free(&cs);
             return -1;
         }
-        if (fscanf(fl, "%4095s", names[i]) != 1) {
+        cs.nnames = i + 1;
+        if (fscanf(fl, "%4095s", cs.names[i]) != 1) {
             fprintf(stderr, "Error reading file name from input file list\n");
             fclose(fl);
+            cli_free(&cs);
             return -1;
         }
         struct stat st;
-        if (stat(names[i], &st) == 0) sizes[i] = (uint64_t)st.st_size;
-        else fprintf(stderr, "Error getting size of file: %s\n", names[i]); /* main.c:294 */
-        files[i].path = names[i];
+        if (stat(cs.names[i], &st) == 0) sizes[i] = (uint64_t)st.st_size;
+        else fprintf(stderr, "Error getting size of file: %s\n", cs.names[i]); /* main.c:294 */
+        files[i].path = cs.names[i];
         files[i].size = sizes[i];
         files[i].id0 = (uint32_t)i; /* main.c:275 */
     }
     fclose(fl);
 
     /* size-balanced shards (main.c:300-328); printed like the reference */
-    uint32_t *order = calloc((size_t)count + 1, sizeof(uint32_t));
-    uint32_t *sb = calloc((size_t)M, sizeof(uint32_t)), *se = calloc((size_t)M, sizeof(uint32_t));
+    cs.order = calloc((size_t)count + 1, sizeof(uint32_t));
+    cs.sb = calloc((size_t)M, sizeof(uint32_t));
+    cs.se = calloc((size_t)M, sizeof(uint32_t));
+    if (!cs.order || !cs.sb || !cs.se) {
+        cli_free(&cs);
+        return 1;
+    }
+    uint32_t *order = cs.order, *sb = cs.sb, *se = cs.se;
     ii_partition(sizes, (uint32_t)count, M, order, sb, se);
     for (int m = 0; m < M; m++) {
         printf("Mapper %d: Files %u to %u\n", m, sb[m], se[m]);
@@ -366,33 +411,30 @@ int main(int argc, char **argv) {
     ii_ctx *single = NULL;
     shard sh[MAXG];
     memset(sh, 0, sizeof(sh));
-    int rc;
+    int rc, reported = 0;
     if (G == 1) {
         rc = ii_open(&single, 0);
-        if (rc != II_OK) {
+        if (rc == II_OK) {
+            /* files in list (= ID) order: postings come out ascending (main.c:217-226) */
+            rc = ii_map_files(single, files, (uint32_t)count, M, NULL);
+            if (rc == II_OK && partials) rc = write_partials(NULL, 0, single, order, nemit);
+            if (rc == II_OK) rc = ii_reduce(single, 1);
+            for (int l = 0; l < II_ALPHABET; l++) owner[l] = single;
+        } else {
             fprintf(stderr, "ii_index: cannot open device: %s\n", ii_strerror(rc));
-            return 1;
+            reported = 1;
         }
-        /* files in list (= ID) order: postings come out ascending (main.c:217-226) */
-        rc = ii_map_files(single, files, (uint32_t)count, M, NULL);
-        if (rc == II_OK && partials) rc = write_partials(NULL, 0, single, order, nemit);
-        if (rc == II_OK) rc = ii_reduce(single, 1);
-        for (int l = 0; l < II_ALPHABET; l++) owner[l] = single;
     } else {
         rc = multi_map(files, sizes, (uint32_t)count, M, G, sh);
         /* partial files while the contexts still hold their input files (before the exchange) */
         if (rc == II_OK && partials) rc = write_partials(sh, G, NULL, order, nemit);
         if (rc == II_OK) rc = multi_exchange(G, sh, owner);
     }
-    if (rc != II_OK) {
-        fprintf(stderr, "ii_index: %s\n", ii_strerror(rc));
-        if (single) ii_close(single);
-        for (int g = 0; g < G; g++)
-            if (sh[g].ctx) ii_close(sh[g].ctx);
-        return 1;
-    }
     int err = 0;
-    if (R > 0) {
+    if (rc != II_OK) {
+        if (!reported) fprintf(stderr, "ii_index: %s\n", ii_strerror(rc));
+        err = 1;
+    } else if (R > 0) {
         pthread_t *th = calloc((size_t)R, sizeof(pthread_t));
         writer_arg *wa = calloc((size_t)R, sizeof(writer_arg));
         for (int r = 0; r < R; r++) {
@@ -412,12 +454,6 @@ int main(int argc, char **argv) {
         free(sh[g].files);
         free(sh[g].local);
     }
-    for (int i = 0; i < count; i++) free(names[i]);
-    free(names);
-    free(files);
-    free(sizes);
-    free(order);
-    free(sb);
-    free(se);
+    cli_free(&cs);
     return err ? 1 : 0;
 }

@@ -1,8 +1,9 @@
 // k1_ablate.hip — timing experiment for the K1 emit kernel (not product code).
-// Times k_tok_emit<kAblate> variants on one synthetic Zipf corpus:
-//   0 full, 16 without the K1c tail (pending tokens), 1 no table probe,
-//   4 no letter histogram, 5 neither, 8 no per-token step (classify + scan +
-//   token list only); and k_tok_count and a read-only pass.
+// Times the K1b kernel body (tok_emit_chunk, ii_kernels.h) with other probe
+// policies on one synthetic Zipf corpus: the product's HotProbe; no probe (the
+// slot is the home slot, no load); a probe of the same shape confined to a
+// region of 2^b slots (2^b * 8 bytes: the cost of the probe instruction when
+// its lines stay in L1 / L2); and k_tok_count and a read-only pass.
 // Usage: k1_ablate [bytes] [files] [vocab]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -48,7 +49,30 @@ float best_of(F f) {
     return best;
 }
 
-template <int A>
+// probe of the same shape as HotProbe's first load, confined to 2^B slots; the slot is the home slot
+template <int B>
+struct RegionProbe {
+    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home, uint64_t) const {
+        if (!fast) return kSlotNone;
+        if (B == 0) return home;
+        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(t.keys + (home & ((1u << B) - 2u)));
+        return q.x == key + 1 ? kSlotNone : home;  // (never equal in practice: keeps the load)
+    }
+};
+template <class Probe>
+__global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
+                                                         const uint64_t* __restrict__ file_start,
+                                                         uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
+                                                         uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
+                                                         uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
+                                                         const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
+                                                         uint64_t long_per, uint32_t narrow_keys) {
+    __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
+    tok_emit_chunk<Probe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf, longs,
+                          long_per, narrow_keys, s_lds);
+}
+
+template <class Probe>
 float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, uint32_t nf, uint64_t* chunk_off,
           Table tab, uint64_t nslots, uint64_t* rec, uint32_t* chist, LongTok* longs, uint64_t lcap, uint64_t nch,
           uint32_t* pend, uint32_t* pcnt) {
@@ -57,14 +81,14 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
     uint32_t* cf;
     const uint32_t wg = (uint32_t)((nch + kWG - 1) / kWG);
     CK(hipMalloc(&cf, 12 * nch));
-    k_chunk_files<<<(uint32_t)((nch + kBlock - 1) / kBlock), kBlock>>>(fstart, fid, nf, nb, kChunk, nch, cf);
+    k_chunk_files<<<(uint32_t)((nch + kBlock - 1) / kBlock), kBlock>>>(fstart, nf, nb, kChunk, nch, cf);
     float best = 1e9;
     for (int it = 0; it < 4; it++) {
         CK(hipMemset(tab.keys, 0, nslots * 8));
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
-        k_tok_emit<A><<<wg, kBlock>>>(d_text, nb, nch, fstart, fid, chunk_off, 0, tab, rec, chist, pend, pcnt, cf,
-                                      longs, lcap / kLongShards, (uint32_t)kNarrowKeys);
+        k_emit_variant<Probe><<<wg, kBlock>>>(d_text, nb, nch, fstart, chunk_off, 0, tab, rec, chist, pend, pcnt, cf,
+                                              longs, lcap / kLongShards, (uint32_t)kNarrowKeys);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -108,12 +132,17 @@ int main(int argc, char** argv) {
     uint32_t *pend, *pcnt;
     CK(hipMalloc(&pend, 4 * T)); CK(hipMalloc(&pcnt, 4 * nch));
     Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters};
-#define RUN(A) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt); \
+#define RUN(A, name) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt); \
     unsigned long long np_ = 0; std::vector<uint32_t> pc_(nch); CK(hipMemcpy(pc_.data(), pcnt, 4 * nch, hipMemcpyDeviceToHost)); \
     for (auto x : pc_) np_ += (x & 0xFFFFu) + (x >> 16); \
-    printf("emit ablate %2d: %.3f ms  pending %llu\n", A, e_, np_); } while (0)
+    printf("emit %-22s: %.3f ms  pending %llu\n", name, e_, np_); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
-    RUN(0); RUN(16); RUN(1); RUN(4); RUN(5); RUN(8);
+    RUN(HotProbe, "full (HotProbe)");
+    RUN(RegionProbe<0>, "no probe");
+    RUN(RegionProbe<12>, "probe 32 KB region");
+    RUN(RegionProbe<17>, "probe 1 MB region");
+    RUN(RegionProbe<18>, "probe 2 MB region");
+    RUN(RegionProbe<20>, "probe 8 MB region");
     printf("count (best of 5): %.3f ms\n", best_of([&] { k_tok_count<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
     printf("read-only (best of 5): %.3f ms\n", best_of([&] { k_read_only<<<wg, kBlock>>>(d_text, nb, nch, chunk); }));
     return 0;

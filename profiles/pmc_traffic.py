@@ -59,7 +59,7 @@ def summarize(out):
     for line in open(bench_log):
         if line.startswith("{"):
             meta = json.loads(line)
-    B = meta.get("config", {}).get("bytes_per_rank")
+    B = meta.get("config", {}).get("bytes_rank0")
     factor = float(os.environ.get("II_PMC_FETCH_FACTOR", "2.0"))
     if B and "ii::k_tok_count" in res and "FETCH_SIZE" in res["ii::k_tok_count"]:
         known = B
@@ -70,6 +70,10 @@ def summarize(out):
             v["read_bytes_per_launch"] = rd
             v["write_bytes_per_launch"] = v["WRITE_SIZE"] * 1024
             v["traffic_bytes_per_launch"] = rd + v["WRITE_SIZE"] * 1024
+            # uncorrected: the correction is for wide coalesced streaming reads; a kernel whose
+            # reads are partly random (K1b's table probes) lies between the two
+            v["read_raw_bytes_per_launch"] = v["FETCH_SIZE"] * 1024
+            v["traffic_raw_bytes_per_launch"] = v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024
     print(json.dumps({"fetch_correction_factor": factor, "bench_line": meta, "kernels": res}, indent=1))
 
 

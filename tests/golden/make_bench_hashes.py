@@ -11,7 +11,11 @@ tests/test_gpu_bench_verify.py asserts the same at full size on the GPU box.
 
 Workloads (bench.py --workload):
   config3        BASELINE configs[2]/[3]: 10 GB Zipf, 10^4 files, vocab 10^6, seed 3
-  config5share   configs[4]'s per-GPU share: 12.5 GB, 1.25*10^5 files, vocab 10^7, seed 5
+  config5share   a configs[4]-sized single-GPU corpus: 12.5 GB, 1.25*10^5 files, vocab 10^7, seed 5
+  config5/share0of8
+                 rank 0's share of BASELINE configs[4] (100 GB, 10^6 files, vocab 10^7, seed 5)
+                 over 8 GPUs: the files ii_partition (main.c:300-323, M = 8) gives shard 0,
+                 with their GLOBAL ids (bench.py --workload config5 --rank-share 0/8)
 """
 import hashlib
 import json
@@ -27,7 +31,17 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 WORKLOADS = {
     "config3": dict(total_bytes=10_000_000_000, nfiles=10_000, vocab=1_000_000, seed=3),
     "config5share": dict(total_bytes=12_500_000_000, nfiles=125_000, vocab=10_000_000, seed=5),
+    "config5": dict(total_bytes=100_000_000_000, nfiles=1_000_000, vocab=10_000_000, seed=5),
 }
+
+
+def share_ids(p, rank, world):
+    """Global ids (ascending) of the files ii_partition gives shard `rank` of `world`."""
+    import ii_ctypes
+    layout = ii_ctypes.zipf_layout(p["total_bytes"], p["nfiles"], p["seed"])
+    sizes = [int(x) for x in (layout[1:] - layout[:-1])]
+    order, sb, se = ii_ctypes.partition(sizes, world)
+    return sorted(order[sb[rank]:se[rank]])
 OUT = os.path.join(HERE, "bench_hashes.json")
 
 
@@ -36,16 +50,24 @@ def main(names):
     from oracle_py import oracle_index
     db = json.load(open(OUT)) if os.path.exists(OUT) else {"workloads": {}}
     for name in names:
-        p = WORKLOADS[name]
+        base, _, share = name.partition("/")
+        p = WORKLOADS[base]
         t0 = time.time()
-        text, off = ii_ctypes.zipf_corpus(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], threads=8)
+        if share:  # "share<r>of<N>": one rank's ii_partition shard, global ids
+            r, n = (int(x) for x in share[len("share"):].split("of"))
+            ids = share_ids(p, r, n)
+            text, off = ii_ctypes.zipf_shard(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], ids, threads=8)
+        else:
+            ids = list(range(p["nfiles"]))
+            text, off = ii_ctypes.zipf_corpus(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], threads=8)
         corpus_sha = hashlib.sha256(memoryview(text)).hexdigest()
         t1 = time.time()
-        res = oracle_index(text, off, list(range(p["nfiles"])))
+        res = oracle_index(text, off, ids, threads=8)
         t2 = time.time()
         letters = {l: {"sha256": hashlib.sha256(v).hexdigest(), "bytes": len(v), "lines": v.count(b"\n")}
                    for l, v in res.items()}
         db["workloads"][name] = {"iigen": p, "corpus_sha256": corpus_sha, "letters": letters,
+                                 "files": len(ids), "bytes": int(off[-1]),
                                  "out_bytes": sum(x["bytes"] for x in letters.values()),
                                  "words": sum(x["lines"] for x in letters.values()),
                                  "oracle_seconds": round(t2 - t1, 1), "gen_seconds": round(t1 - t0, 1)}
@@ -56,4 +78,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(WORKLOADS))
+    main(sys.argv[1:] or ["config3", "config5share", "config5/share0of8"])

@@ -1,7 +1,7 @@
 """GPU: the benchmark corpora at FULL size against the oracle — every letter
-of the index of BASELINE configs[2] (10 GB, 10^4 files, vocab 10^6, seed 3)
-and of configs[4]'s per-GPU share (12.5 GB, 1.25*10^5 files, vocab 10^7,
-seed 5) hashed and compared with tests/golden/bench_hashes.json (made by the
+of the index of BASELINE configs[2] (10 GB, 10^4 files, vocab 10^6, seed 3),
+of a configs[4]-sized corpus (12.5 GB, 1.25*10^5 files, vocab 10^7, seed 5)
+and of rank 0's ii_partition share of configs[4] over 8 GPUs, hashed and compared with tests/golden/bench_hashes.json (made by the
 oracle in the build container, tests/golden/make_bench_hashes.py)."""
 import hashlib
 import json
@@ -17,24 +17,43 @@ pytestmark = pytest.mark.gpu
 DB = json.load(open(os.path.join(GOLDEN, "bench_hashes.json")))["workloads"]
 
 
-@pytest.mark.parametrize("name", ["config3", "config5share"])
+def share_ids(p, rank, world):
+    """Global ids of the files ii_partition (main.c:300-323, M = world) gives shard `rank`."""
+    layout = ii_ctypes.zipf_layout(p["total_bytes"], p["nfiles"], p["seed"])
+    order, sb, se = ii_ctypes.partition([int(x) for x in (layout[1:] - layout[:-1])], world)
+    return sorted(order[sb[rank]:se[rank]])
+
+
+@pytest.mark.parametrize("name", ["config3", "config5share", "config5/share0of8"])
 def test_full_size_index_matches_oracle(name):
+    """config5/share0of8: rank 0's share of configs[4] over 8 GPUs (1.25*10^5
+    files whose global ids span [0, 10^6)) — the shape a real rank indexes; its
+    records carry 17-bit shard-local file indices, so the packed sort runs."""
     import torch
     if name not in DB:
         pytest.skip("no oracle hashes for %s" % name)
     w = DB[name]
     p = w["iigen"]
-    text, off = ii_ctypes.zipf_corpus(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], threads=16)
+    _, _, share = name.partition("/")
+    if share:
+        r, g = (int(x) for x in share[len("share"):].split("of"))
+        ids = share_ids(p, r, g)
+        text, off = ii_ctypes.zipf_shard(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], ids, threads=16)
+    else:
+        ids = list(range(p["nfiles"]))
+        text, off = ii_ctypes.zipf_corpus(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], threads=16)
     n = int(off[-1])
     d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     d[:n].copy_(torch.from_numpy(text))
     torch.cuda.synchronize()
     del text
     with ii_ctypes.Index(0) as ix:
-        ix.map_device(d.data_ptr(), n, off[:-1].tolist(), list(range(p["nfiles"])))
+        ix.map_device(d.data_ptr(), n, off[:-1].tolist(), ids)
         ix.reduce(copy_text=True)
         st = ix.stats()
         assert st.words == w["words"] and st.out_bytes == w["out_bytes"]
         bad = [l for l in w["letters"] if hashlib.sha256(ix.letter_text(ord(l) - 97)).hexdigest()
                != w["letters"][l]["sha256"]]
+        if share:
+            assert st.sort_packed == 1
     assert not bad, "letters differ from the oracle: %s" % bad

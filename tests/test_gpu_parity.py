@@ -345,19 +345,22 @@ def test_logical_shards_balanced_letters(case, G):
     assert_same(shard_and_merge(text, off, G, balanced=True), expected, "%s G=%d balanced" % (case, G))
 
 
-def test_config5_shape_vs_oracle():
-    # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 files (far beyond the
-    # reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), ~3 KB files
-    nf = 100_000
+@pytest.mark.parametrize("nf,packed", [(140_000, 1), (300_000, 0)])
+def test_config5_shape_vs_oracle(nf, packed):
+    # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 1.4*10^5 / 3*10^5 files (far
+    # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-2 KB
+    # files.  V > 3*10^6 gives 22-bit word ids; 18-bit file indices leave the packed sort an 8-bit top
+    # digit (W + F - 32 = 8), 19-bit ones do not pack (the u64 passes run)
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
     with ii_ctypes.Index(0) as ix:
         ix.map_host(t, off.tolist(), ids)
         ix.reduce()
-        assert_same(ix.letters(), exp, "300 MB, 1e5 files, vocab 1e7")
+        assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7" % nf)
         st = ix.stats()
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
+    assert st.sort_packed == packed
 
 
 def test_large_vocab_vs_oracle_both_key_modes():
@@ -384,12 +387,13 @@ def test_large_vocab_vs_oracle_both_key_modes():
 def test_packed_sort_forms_vs_oracle():
     """The token sort's packed form (ii_prims.h "Packed token sort": MSD buckets
     of u32 records, two bucket-local onesweep passes) against the u64 form
-    (II_PACKED_SORT=0) and the oracle: 7-bit top digit (ids of 10 bits), 8-bit
-    top digit (ids spread to 19 bits: W + F - 32 = 8) and ids too wide to pack
-    (22 bits: the u64 form runs)."""
+    (II_PACKED_SORT=0) and the oracle, for dense ids and for ids spread to 19
+    and 22 bits: the records carry shard-local file indices (10 bits for 700
+    files, k_chunk_files), so every shape packs and K3 maps the indices back
+    to the ids (k_uniq_sweep fmap) in both forms."""
     t, off = ii_ctypes.zipf_corpus(48_000_000, 700, 300_000, 23, threads=8)
     off = off.tolist()
-    for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 0)]:
+    for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 1)]:
         exp = oracle_index(t, off, ids)
         for env in [None, "0"]:
             if env is not None:
@@ -404,3 +408,73 @@ def test_packed_sort_forms_vs_oracle():
                     assert st.sort_bytes > 0
             finally:
                 os.environ.pop("II_PACKED_SORT", None)
+
+
+def test_global_ids_of_a_share_stay_packed():
+    """A rank's ii_partition share (main.c:300-323): 2000 files whose global ids
+    span [0, 10^6) — the shape of a configs[4] rank.  The records carry 11-bit
+    shard-local indices, so the packed sort runs; postings print the global ids."""
+    t, off = ii_ctypes.zipf_corpus(40_000_000, 2000, 1_000_000, 41, threads=8)
+    rng = random.Random(41)
+    ids = sorted(rng.sample(range(1_000_000), 2000))
+    exp = oracle_index(t, off, ids)
+    with ii_ctypes.Index(0) as ix:
+        ix.map_host(t, off.tolist(), ids)
+        ix.reduce()
+        assert_same(ix.letters(), exp, "global ids of a share")
+        assert ix.stats().sort_packed == 1
+
+
+TINY = [
+    ([b"a"], [0]),
+    ([b"a b"], [4]),
+    ([b"b a c"], [0]),
+    ([b"", b"x"], [0, 1]),
+    ([b"", b"", b""], [0, 1, 2]),
+    ([b"zz zz zz"], [9]),
+    ([b"", b"q", b""], [1, 5, 6]),
+    ([b"y", b"y", b"y"], [0, 2, 3]),
+    ([b"a", b"", b"b"], [0, 1, 2]),
+]
+
+
+@pytest.mark.parametrize("k", range(len(TINY)))
+def test_tiny_shapes_vs_oracle(idx, k):
+    """1-3 records, empty files, buckets left empty: the packed sort's geometry
+    and K3 on the smallest inputs (the round-2 fault on 1-file / empty shards)."""
+    files, ids = TINY[k]
+    text = b"\n".join(files)
+    off = [0]
+    for i, f in enumerate(files):
+        off.append(off[-1] + len(f) + (1 if i + 1 < len(files) else 0))
+    idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(text, off, ids), "tiny %d" % k)
+
+
+@pytest.mark.parametrize("k", [0, 2, 4, 6, 8])
+def test_tiny_shapes_logical_shards(k):
+    # the same through the exchange: shards of one file, of one empty file, and empty shards
+    files, ids = TINY[k]
+    text = b"\n".join(files)
+    off = [0]
+    for i, f in enumerate(files):
+        off.append(off[-1] + len(f) + (1 if i + 1 < len(files) else 0))
+    exp = oracle_index(text, off, list(range(len(files))))  # (shard_and_merge numbers files by list position)
+    assert_same(shard_and_merge(text, off, 3), exp, "tiny %d G=3" % k)
+
+
+def test_k3_lookback_timeout_is_an_error():
+    """K3 flags a look-back that never resolved (kLbTimeout) instead of
+    hanging; the host must turn the flag into II_ERR_INTERNAL, not return the
+    wrong pairs (II_TEST_LB_TIMEOUT=1 raises the flag after K3)."""
+    text, off, ids, _ = case_arrays("config2")
+    os.environ["II_TEST_LB_TIMEOUT"] = "1"
+    try:
+        with ii_ctypes.Index(0) as ix:
+            ix.map_host(text, off, ids)
+            with pytest.raises(ii_ctypes.IIError) as e:
+                ix.reduce()
+            assert e.value.code == -7
+    finally:
+        os.environ.pop("II_TEST_LB_TIMEOUT", None)
