@@ -703,7 +703,8 @@ def main():
             "counts": {"tokens": st.tokens, "pairs": st.pairs, "words": st.words, "long_tokens": st.long_tokens,
                        "out_bytes": st.out_bytes, "sort_passes": st.sort_passes, "table_cap": st.table_cap,
                        "resolved_tokens": st.resolved_tokens, "sorted_records": st.sorted_records,
-                       "sort_packed": st.sort_packed, "files": len(ids)},
+                       "sort_packed": st.sort_packed, "sort_key_bits": st.sort_key_bits,
+                       "sort_id_bits": st.sort_id_bits, "files": len(ids)},
             "export": export_leg,
             "output_letter_sha256": letter_sha if letter_sha else None,
             "libii_sha16": build,

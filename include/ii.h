@@ -96,6 +96,8 @@ typedef struct {
      * every scatter / onesweep launch and the packed form's bucket histogram) */
     uint64_t sort_bytes;
     uint32_t sort_packed;  /* 1: the packed form (u32 records in buckets, ii_prims.h) ran */
+    uint32_t sort_key_bits;  /* W: bits of the token sort's word keys */
+    uint32_t sort_id_bits;   /* F: bits of the records' shard-local file indices (packed form: W + F - 32 <= 8) */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

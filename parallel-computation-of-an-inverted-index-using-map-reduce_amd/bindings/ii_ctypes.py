@@ -41,6 +41,7 @@ class Stats(ctypes.Structure):
         ("sort0_ms", ctypes.c_double), ("sort0_bytes", ctypes.c_uint64),
         ("io_ms", ctypes.c_double), ("io_bytes", ctypes.c_uint64),
         ("sort_bytes", ctypes.c_uint64), ("sort_packed", ctypes.c_uint32),
+        ("sort_key_bits", ctypes.c_uint32), ("sort_id_bits", ctypes.c_uint32),
     ]
 
     def as_dict(self):

@@ -105,6 +105,7 @@ struct ii_ctx {
     hipEvent_t ev_c0[2] = {};  // around k_sort0_compact
     uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
     bool sort_packed = false;  // the last token sort ran in the packed form (run_sort_packed)
+    int sort_W = 0, sort_F = 0;  // its key / file-index bits
     uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
     // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
     uint32_t pk_nb = 0, pk_ntb = 0;
@@ -1188,6 +1189,8 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     // the records carry shard-local file indices (k_chunk_files): F bits for this map's files
     const int F = std::max(1, bitlen(c->nfiles ? c->nfiles - 1 : 0));
     c->sort_packed = false;
+    c->sort_W = lb;
+    c->sort_F = F;
     const int m = packed_top_bits(lb, F);
     if (m)
         CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
@@ -1651,6 +1654,8 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: bytes read + written
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
+        s.sort_key_bits = (uint32_t)c->sort_W;
+        s.sort_id_bits = (uint32_t)c->sort_F;
         s.sorted_records = c->T_sorted;
         if (c->c0_bytes) {
             s.sort0_ms = ev_ms(c->ev_c0[0], c->ev_c0[1]);

@@ -59,6 +59,27 @@ struct RegionProbe {
         return q.x == key + 1 ? kSlotNone : home;  // (never equal in practice: keeps the load)
     }
 };
+// HotProbe with the bucket's first NP slot pairs (in probe order) loaded at once: one round trip
+template <int NP>
+struct WideProbe {
+    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
+                                                   uint64_t pos) const {
+        if (!fast) return kSlotNone;
+        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
+        ulonglong2 q[NP];
+#pragma unroll
+        for (int j = 0; j < NP; j++)
+            q[j] = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2 * j) & (kBucket - 2)));
+        uint32_t match = 0, empty = 0;
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            match |= ((uint32_t)(q[j].x == key) << (2 * j)) | ((uint32_t)(q[j].y == key) << (2 * j + 1));
+            empty |= ((uint32_t)(q[j].x == 0ull) << (2 * j)) | ((uint32_t)(q[j].y == 0ull) << (2 * j + 1));
+        }
+        return bucket_resolve(t, match, empty, key, bbase, start, pos);
+    }
+};
+
 template <class Probe>
 __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                          const uint64_t* __restrict__ file_start,
@@ -138,6 +159,9 @@ int main(int argc, char** argv) {
     printf("emit %-22s: %.3f ms  pending %llu\n", name, e_, np_); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(HotProbe, "full (HotProbe)");
+    RUN(WideProbe<2>, "two pairs at once");
+    RUN(WideProbe<4>, "whole bucket at once");
+    RUN(HotProbe, "full (HotProbe) again");
     RUN(RegionProbe<0>, "no probe");
     RUN(RegionProbe<12>, "probe 32 KB region");
     RUN(RegionProbe<17>, "probe 1 MB region");

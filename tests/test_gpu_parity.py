@@ -345,12 +345,12 @@ def test_logical_shards_balanced_letters(case, G):
     assert_same(shard_and_merge(text, off, G, balanced=True), expected, "%s G=%d balanced" % (case, G))
 
 
-@pytest.mark.parametrize("nf,packed", [(140_000, 1), (300_000, 0)])
-def test_config5_shape_vs_oracle(nf, packed):
-    # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 1.4*10^5 / 3*10^5 files (far
-    # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-2 KB
-    # files.  V > 3*10^6 gives 22-bit word ids; 18-bit file indices leave the packed sort an 8-bit top
-    # digit (W + F - 32 = 8), 19-bit ones do not pack (the u64 passes run)
+@pytest.mark.parametrize("nf", [100_000, 300_000])
+def test_config5_shape_vs_oracle(nf):
+    # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 / 3*10^5 files (far
+    # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-3 KB
+    # files.  The packed sort runs when W + F - 32 <= 8 (W word-id bits, F file-index bits): 17-bit
+    # indices pack with the 23-bit word ids of this vocabulary, 19-bit ones take the u64 passes
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
@@ -360,7 +360,8 @@ def test_config5_shape_vs_oracle(nf, packed):
         assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7" % nf)
         st = ix.stats()
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
-    assert st.sort_packed == packed
+    assert st.sort_packed == (st.sort_key_bits + st.sort_id_bits - 32 <= 8)
+    assert st.sort_id_bits == (nf - 1).bit_length()
 
 
 def test_large_vocab_vs_oracle_both_key_modes():
