@@ -564,11 +564,9 @@ def main():
             torch.cuda.synchronize()
             if it >= a.warmup:
                 ts.append(time.perf_counter() - t1)
-        est = idx.stats()
         export_leg = {"what": "map + ii_reduce_local + ii_export_plan + ii_export (%d parts, the reference's "
                               "reducer letters)" % parts, "ms": round(statistics.median(ts) * 1e3, 3),
-                      "GBps": round(total_bytes / statistics.median(ts) / 1e9, 3), "send_bytes": int(sum(sizes)),
-                      "sort_packed": est.sort_packed, "sort_passes": est.sort_passes}
+                      "GBps": round(total_bytes / statistics.median(ts) / 1e9, 3), "send_bytes": int(sum(sizes))}
 
     # ---- outside the timed region: the index itself, against the oracle's hashes
     verified, verify_note, letter_sha = None, None, {}

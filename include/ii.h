@@ -192,6 +192,9 @@ int ii_letter_load(ii_ctx *ctx, uint64_t pairs[II_ALPHABET]);
 int ii_balanced_letters(const uint64_t weight[II_ALPHABET], int nparts, int *letter_lo, int *letter_hi);
 int ii_export_plan_ranges(ii_ctx *ctx, int nparts, const int *letter_lo, const int *letter_hi, uint64_t *seg_bytes);
 int ii_export(ii_ctx *ctx, int nparts, void *d_send, const uint64_t *send_off);
+/* ii_import: segment s comes from source s (0 .. nparts-1, any order of file
+ * ids across sources), and every file id belongs to ONE source — files are
+ * sharded, not replicated (main.c:300-323 gives each file one mapper). */
 int ii_import(ii_ctx *ctx, int nparts, const void *d_recv, const uint64_t *recv_off, uint32_t id_bound);
 
 /* Text of <letter>.txt (letter 0..25 = 'a'..'z'), valid until the next call. */

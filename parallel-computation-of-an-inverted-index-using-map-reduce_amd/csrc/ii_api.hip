@@ -62,6 +62,7 @@ struct ii_ctx {
     DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
     DBuf uniq_x, pstart_x;  // exchange after a word-id reduce: the pairs in lexid order (letter_points)
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
+    DBuf moff;              // ii_import merge of interleaved sources: per (word, source) merged offset
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
@@ -602,7 +603,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
-                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk};
+                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk, &c->moff};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -1476,13 +1477,16 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         pbase += np;
     }
     HIPCK(hipGetLastError());
-    // (lexid, id0) order: LSD over the id bits, then the word bits
+    // (lexid, id0) order.  Every source's pairs arrive sorted by (word, id0)
+    // (K3 order; local and global lexicographic ids agree in order), so the
+    // owner merges per (word, source) runs (k_merge_runs): when the sources'
+    // id ranges ascend without overlap (ranks owning contiguous file ranges)
+    // the merged order is (word, source) — k_merge_scatter moves whole runs;
+    // otherwise (ii_partition's interleaved shards) k_merge_ids places every
+    // pair by binary searches of the word's other runs.  II_IMPORT_ID_SORT=1
+    // (test knob) sorts instead: LSD over the id bits, then the word bits.
     int p1 = 0, p2 = 0;
     c->n_sc = 0;
-    // Every source's pairs arrive sorted by (word, id0) (K3 order; local and
-    // global lexicographic ids agree in order).  When the sources' id ranges
-    // ascend without overlap (ranks owning contiguous file ranges), a stable
-    // sort by word alone leaves (word, id0) order: the id pass is skipped.
     bool ordered = true;
     uint64_t prev_hi1 = 0;
     for (int s = 0; s < nparts && ordered; s++) {
@@ -1491,8 +1495,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
         prev_hi1 = hi1;
     }
-    if (ordered && !getenv("II_IMPORT_ID_SORT")) {
-        // merge the sorted segments by (word, source) runs: k_merge_runs / k_merge_scatter
+    if (!getenv("II_IMPORT_ID_SORT")) {
         const uint64_t nk = c->V * (uint64_t)nparts;
         CK(grow(c->mstart, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
         CK(grow(c->mend, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
@@ -1507,21 +1510,30 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
                     r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me);
             pb += np;
         }
-        CK(run_scan(c, OpMergeRuns{ms, me}, nk, nullptr));
+        uint64_t* mo = nullptr;
+        if (ordered) {
+            CK(run_scan(c, OpMergeRuns{ms, me}, nk, nullptr));
+        } else {
+            CK(grow(c->moff, sizeof(uint64_t) * (nk + 1)));
+            mo = P_<uint64_t>(c->moff);
+            CK(run_scan(c, OpRunOffsets{ms, me, mo}, nk, mo + nk));
+        }
         pb = 0;
         for (int s = 0; s < nparts; s++) {
             const uint64_t np = hdr[8 * s + 2];
-            if (np)
+            if (np && ordered)
                 k_merge_scatter<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
                     r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me, r2);
+            else if (np)
+                k_merge_ids<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
+                    r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me, mo, r2);
             pb += np;
         }
         HIPCK(hipGetLastError());
         std::swap(r, r2);
     } else {
-        if (!ordered || getenv("II_IMPORT_ID_SORT"))
-            CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false,
-                        &p1));
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false,
+                    &p1));
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));

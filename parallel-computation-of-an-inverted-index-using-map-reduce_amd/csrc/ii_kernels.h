@@ -790,6 +790,9 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                 key = rec[cbase + (narrow ? kNarrowKeys + i : jr)];
             }
             slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
+            // a word K1b claimed without waiting (fire-and-forget CAS) has no representative yet: any of
+            // its occurrences is one (exact <= 12-letter keys)
+            if (!kSlow && slot < kHotSlots) tab.rep[slot] = pos;
             if (narrow) {
                 reinterpret_cast<uint32_t*>(rec + cbase)[jr] = (uint32_t)slot;
             } else {
@@ -2119,6 +2122,47 @@ __global__ __launch_bounds__(kBlock) void k_merge_runs(const uint64_t* __restric
         const uint64_t k = (uint64_t)w * G + g;
         if (i == 0 || (uint32_t)(r[pb + i - 1] >> 32) != w) rstart[k] = pb + i;
         if (i + 1 == np || (uint32_t)(r[pb + i + 1] >> 32) != w) rend[k] = pb + i + 1;
+    }
+}
+// run lengths (rend = 0: no run) -> exclusive offsets in moff (rstart / rend kept)
+struct OpRunOffsets {
+    const uint64_t* rstart;
+    const uint64_t* rend;
+    uint64_t* moff;
+    __device__ uint64_t value(uint64_t i) const { return rend[i] ? rend[i] - rstart[i] : 0; }
+    __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { moff[i] = ex; }
+};
+// Owner-side merge when the sources' id ranges interleave (ii_partition's
+// size-sorted shards, main.c:300-323): word w's pairs arrive as up to G runs,
+// one per source, each sorted by id0, and no id0 occurs in two sources (a file
+// belongs to one shard).  A pair's place in the word's merged run is its index
+// in its own run plus, for every other source, the number of that source's
+// ids below its own — a binary search of that run, whose lines the
+// neighbouring lanes share; the word's block starts at moff[w * G].  One pass
+// over the pairs of source g instead of the owner's id and word radix passes.
+__global__ __launch_bounds__(kBlock) void k_merge_ids(const uint64_t* __restrict__ r, uint64_t pb, uint64_t np,
+                                                      uint32_t G, uint32_t g, const uint64_t* __restrict__ rstart,
+                                                      const uint64_t* __restrict__ rend,
+                                                      const uint64_t* __restrict__ moff, uint64_t* __restrict__ out) {
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(r);  // id0 = the low dword of a pair
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t v = r[pb + i];
+        const uint32_t x = (uint32_t)v;
+        const uint64_t k0 = (uint64_t)(uint32_t)(v >> 32) * G;
+        uint64_t dst = moff[k0] + (pb + i - rstart[k0 + g]);
+        for (uint32_t s = 0; s < G; s++) {
+            const uint64_t e = s == g ? 0 : rend[k0 + s];
+            if (!e) continue;  // own run, or no run of this word in source s
+            const uint64_t b = rstart[k0 + s];
+            uint64_t lo = b, hi = e;  // first pair of the run with id0 >= x
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (r32[2 * mid] < x) lo = mid + 1;
+                else hi = mid;
+            }
+            dst += lo - b;
+        }
+        out[dst] = v;
     }
 }
 // run lengths (rend = 0: no run) -> exclusive offsets, in place in rend

@@ -11,6 +11,8 @@ import, order + format — each timed across all G contexts.
 interleaved = 1: shard g owns files g, g + G, g + 2G, ... (the id ranges of
 the sources overlap, as with bench.py's ii_partition shards, so the owners
 sort their merged pairs instead of merging ordered runs).
+owner_ms_*: the owners' device time per ii_import phase (hipEvents inside
+libii: word tokenisation, dictionary, merge / sort, unique) and order / format.
 """
 import json
 import os
@@ -83,11 +85,15 @@ def main():
             t0 = time.perf_counter()
             ix.reduce(copy_text=False)
             lap("order_format", t0)
+            # the owner's device-side phases of ii_import (+ order / format): events inside libii
+            st = ix.stats()
+            for k in ("ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format"):
+                ph["owner_" + k] = ph.get("owner_" + k, 0.0) + getattr(st, k)
         ph["exchange_bytes"] = sum(sum(s[1]) for s in sends)
         if it:
             res.append(ph)
     avg = {k: round(sum(r[k] for r in res) / len(res), 2) for k in res[0]}
-    avg["per_shard_ms"] = {k: round(v / G, 2) for k, v in avg.items() if k != "exchange_bytes"}
+    avg["per_shard_ms"] = {k: round(v / G, 3) for k, v in avg.items() if k != "exchange_bytes"}
     print(json.dumps({"G": G, "bytes_per_shard": nb, "interleaved_ids": inter, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
                       "phases_ms_all_shards": avg}))
     for ix in idxs:

@@ -80,6 +80,46 @@ struct WideProbe {
     }
 };
 
+// the home slot's pair only: a word found there, or claimed there (kClaim), resolves; every other
+// token goes to the K1c tail (no second round trip in the rounds)
+template <bool kClaim>
+struct PairProbe {
+    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
+                                                   uint64_t pos) const {
+        if (!fast) return kSlotNone;
+        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
+        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
+        const uint32_t match = (uint32_t)(q.x == key) | ((uint32_t)(q.y == key) << 1);
+        const uint32_t empty = (uint32_t)(q.x == 0ull) | ((uint32_t)(q.y == 0ull) << 1);
+        if (!kClaim && !match) return kSlotNone;
+        return bucket_resolve(t, match, empty, key, bbase, start, pos);
+    }
+};
+
+// HotProbe whose claims do not wait: a word found in the two pairs resolves; a word whose pairs have
+// an empty slot claims the first one with a CAS whose result nobody waits for, and goes to the K1c
+// tail (table_find finds it there, or places it where the CAS lost)
+struct LazyProbe {
+    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
+                                                   uint64_t pos) const {
+        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
+        ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
+        if (fast) qa = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
+        uint32_t match = (uint32_t)(qa.x == key) | ((uint32_t)(qa.y == key) << 1);
+        uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
+        if (fast && !(match | empty)) {
+            qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
+            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
+            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
+        }
+        if (!fast) return kSlotNone;
+        if (match) return bbase + ((start + __builtin_ctz(match)) & (kBucket - 1));
+        if (empty) atomicCAS(&t.keys[bbase + ((start + __builtin_ctz(empty)) & (kBucket - 1))], 0ull,
+                             (unsigned long long)key);
+        return kSlotNone;
+    }
+};
+
 template <class Probe>
 __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                          const uint64_t* __restrict__ file_start,
@@ -159,9 +199,9 @@ int main(int argc, char** argv) {
     printf("emit %-22s: %.3f ms  pending %llu\n", name, e_, np_); } while (0)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(HotProbe, "full (HotProbe)");
-    RUN(WideProbe<2>, "two pairs at once");
-    RUN(WideProbe<4>, "whole bucket at once");
+    RUN(LazyProbe, "claims without waiting");
     RUN(HotProbe, "full (HotProbe) again");
+    RUN(LazyProbe, "claims without waiting again");
     RUN(RegionProbe<0>, "no probe");
     RUN(RegionProbe<12>, "probe 32 KB region");
     RUN(RegionProbe<17>, "probe 1 MB region");
