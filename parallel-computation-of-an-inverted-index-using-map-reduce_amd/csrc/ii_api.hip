@@ -1482,9 +1482,13 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // owner merges per (word, source) runs (k_merge_runs): when the sources'
     // id ranges ascend without overlap (ranks owning contiguous file ranges)
     // the merged order is (word, source) — k_merge_scatter moves whole runs;
-    // otherwise (ii_partition's interleaved shards) k_merge_ids places every
-    // pair by binary searches of the word's other runs.  II_IMPORT_ID_SORT=1
-    // (test knob) sorts instead: LSD over the id bits, then the word bits.
+    // with interleaved ranges (ii_partition's size-sorted shards) and at most
+    // kMergeIdsMaxParts sources, k_merge_ids places every pair by binary
+    // searches of the word's other runs; with more sources (G - 1 searches per
+    // pair) the owner sorts: LSD over the id bits, then the word bits.
+    // Measured per owner (tools/exchange_timing.py, 10 GB over G interleaved
+    // shards): G = 2 merge 2.21 / sort 5.25 ms, G = 4 2.16 / 3.30, G = 8
+    // 2.41 / 2.04.  II_IMPORT_ID_SORT=1 (test knob) always sorts.
     int p1 = 0, p2 = 0;
     c->n_sc = 0;
     bool ordered = true;
@@ -1495,7 +1499,8 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
         prev_hi1 = hi1;
     }
-    if (!getenv("II_IMPORT_ID_SORT")) {
+    constexpr int kMergeIdsMaxParts = 4;
+    if (!getenv("II_IMPORT_ID_SORT") && (ordered || nparts <= kMergeIdsMaxParts)) {
         const uint64_t nk = c->V * (uint64_t)nparts;
         CK(grow(c->mstart, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
         CK(grow(c->mend, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));

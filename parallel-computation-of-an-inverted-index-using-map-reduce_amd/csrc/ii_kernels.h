@@ -790,9 +790,6 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                 key = rec[cbase + (narrow ? kNarrowKeys + i : jr)];
             }
             slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-            // a word K1b claimed without waiting (fire-and-forget CAS) has no representative yet: any of
-            // its occurrences is one (exact <= 12-letter keys)
-            if (!kSlow && slot < kHotSlots) tab.rep[slot] = pos;
             if (narrow) {
                 reinterpret_cast<uint32_t*>(rec + cbase)[jr] = (uint32_t)slot;
             } else {

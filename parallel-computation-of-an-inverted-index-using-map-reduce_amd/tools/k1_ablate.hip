@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <vector>
 #include "../csrc/ii_kernels.h"
 using namespace ii;
@@ -80,45 +81,31 @@ struct WideProbe {
     }
 };
 
-// the home slot's pair only: a word found there, or claimed there (kClaim), resolves; every other
-// token goes to the K1c tail (no second round trip in the rounds)
-template <bool kClaim>
-struct PairProbe {
+// A small direct-mapped cache in front of HotProbe: (key, slot) of the most frequent hot words
+// (found by counting a previous run's records, tools only), 2^B entries of 16 B; a miss takes HotProbe.
+// What a sampling pre-pass could buy: the share of tokens served by an L1 / L2-resident table.
+__device__ const ulonglong2* g_small = nullptr;
+__host__ __device__ __forceinline__ uint32_t small_hash(uint64_t key) {
+    uint32_t h = (uint32_t)(key >> 32) * 0x9E3779B1u ^ (uint32_t)key * 0x85EBCA77u;
+    return h ^ (h >> 15);
+}
+template <int B>
+struct SmallProbe {
     __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
                                                    uint64_t pos) const {
-        if (!fast) return kSlotNone;
-        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
-        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
-        const uint32_t match = (uint32_t)(q.x == key) | ((uint32_t)(q.y == key) << 1);
-        const uint32_t empty = (uint32_t)(q.x == 0ull) | ((uint32_t)(q.y == 0ull) << 1);
-        if (!kClaim && !match) return kSlotNone;
-        return bucket_resolve(t, match, empty, key, bbase, start, pos);
+        ulonglong2 e = make_ulonglong2(0ull, 0ull);
+        if (fast) e = g_small[small_hash(key) & ((1u << B) - 1u)];
+        if (fast && e.x == key) return (uint32_t)e.y;
+        return HotProbe()(t, fast && e.x != key, key, home, pos);
     }
 };
 
-// HotProbe whose claims do not wait: a word found in the two pairs resolves; a word whose pairs have
-// an empty slot claims the first one with a CAS whose result nobody waits for, and goes to the K1c
-// tail (table_find finds it there, or places it where the CAS lost)
-struct LazyProbe {
-    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
-                                                   uint64_t pos) const {
-        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
-        ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
-        if (fast) qa = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
-        uint32_t match = (uint32_t)(qa.x == key) | ((uint32_t)(qa.y == key) << 1);
-        uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
-        if (fast && !(match | empty)) {
-            qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
-            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
-            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
-        }
-        if (!fast) return kSlotNone;
-        if (match) return bbase + ((start + __builtin_ctz(match)) & (kBucket - 1));
-        if (empty) atomicCAS(&t.keys[bbase + ((start + __builtin_ctz(empty)) & (kBucket - 1))], 0ull,
-                             (unsigned long long)key);
-        return kSlotNone;
+__global__ void k_slot_hist(const uint64_t* __restrict__ rec, uint64_t n, uint32_t* __restrict__ cnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s = rec[i] >> 32;
+        if (s < kHotSlots) atomicAdd(&cnt[s], 1u);
     }
-};
+}
 
 template <class Probe>
 __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
@@ -136,7 +123,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __res
 template <class Probe>
 float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, uint32_t nf, uint64_t* chunk_off,
           Table tab, uint64_t nslots, uint64_t* rec, uint32_t* chist, LongTok* longs, uint64_t lcap, uint64_t nch,
-          uint32_t* pend, uint32_t* pcnt) {
+          uint32_t* pend, uint32_t* pcnt, bool warm = false) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     uint32_t* cf;
@@ -145,7 +132,7 @@ float run(const uint8_t* d_text, uint64_t nb, uint64_t* fstart, uint32_t* fid, u
     k_chunk_files<<<(uint32_t)((nch + kBlock - 1) / kBlock), kBlock>>>(fstart, nf, nb, kChunk, nch, cf);
     float best = 1e9;
     for (int it = 0; it < 4; it++) {
-        CK(hipMemset(tab.keys, 0, nslots * 8));
+        if (!warm) CK(hipMemset(tab.keys, 0, nslots * 8));  // warm: the words of earlier runs stay
         CK(hipMemset(tab.counters, 0, 8 * C_NUM));
         CK(hipEventRecord(a));
         k_emit_variant<Probe><<<wg, kBlock>>>(d_text, nb, nch, fstart, chunk_off, 0, tab, rec, chist, pend, pcnt, cf,
@@ -193,15 +180,48 @@ int main(int argc, char** argv) {
     uint32_t *pend, *pcnt;
     CK(hipMalloc(&pend, 4 * T)); CK(hipMalloc(&pcnt, 4 * nch));
     Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters};
-#define RUN(A, name) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt); \
+#define RUNW(A, name, warm) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt, warm); \
     unsigned long long np_ = 0; std::vector<uint32_t> pc_(nch); CK(hipMemcpy(pc_.data(), pcnt, 4 * nch, hipMemcpyDeviceToHost)); \
     for (auto x : pc_) np_ += (x & 0xFFFFu) + (x >> 16); \
-    printf("emit %-22s: %.3f ms  pending %llu\n", name, e_, np_); } while (0)
+    printf("emit %-30s: %.3f ms  pending %llu\n", name, e_, np_); } while (0)
+#define RUN(A, name) RUNW(A, name, false)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(HotProbe, "full (HotProbe)");
-    RUN(LazyProbe, "claims without waiting");
-    RUN(HotProbe, "full (HotProbe) again");
-    RUN(LazyProbe, "claims without waiting again");
+    RUN(WideProbe<2>, "two pairs at once");
+    // small front tables of the most frequent hot words (counted from the records of a warm run)
+    RUNW(HotProbe, "HotProbe, warm table", true);
+    {
+        uint32_t* d_cnt;
+        CK(hipMalloc(&d_cnt, 4 * kHotSlots));
+        CK(hipMemset(d_cnt, 0, 4 * kHotSlots));
+        k_slot_hist<<<4096, 256>>>(rec, T, d_cnt);
+        std::vector<uint32_t> hc(kHotSlots);
+        std::vector<unsigned long long> hk(kHotSlots);
+        CK(hipMemcpy(hc.data(), d_cnt, 4 * kHotSlots, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hk.data(), keys, 8 * kHotSlots, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> order(kHotSlots);
+        for (uint32_t i = 0; i < kHotSlots; i++) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hc[x] > hc[y]; });
+        ulonglong2* d_small;
+        CK(hipMalloc(&d_small, 16ull << 14));
+        for (int B = 11; B <= 14; B++) {
+            std::vector<ulonglong2> tbl(1u << B, make_ulonglong2(0ull, 0ull));
+            uint64_t served = 0;
+            for (uint32_t j = 0; j < (1u << B) && hc[order[j]]; j++) {  // most frequent first; a taken entry keeps its word
+                const uint32_t sl = order[j];
+                ulonglong2& e = tbl[small_hash(hk[sl]) & ((1u << B) - 1u)];
+                if (e.x == 0ull) { e = make_ulonglong2(hk[sl], sl); served += hc[sl]; }
+            }
+            CK(hipMemcpy(d_small, tbl.data(), 16ull << B, hipMemcpyHostToDevice));
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_small), &d_small, sizeof(d_small)));
+            printf("small table 2^%d entries (%u KB): %.1f %% of tokens\n", B, 16u << B >> 10, 100.0 * served / T);
+            if (B == 11) RUNW(SmallProbe<11>, "small 2^11 + HotProbe, warm", true);
+            if (B == 12) RUNW(SmallProbe<12>, "small 2^12 + HotProbe, warm", true);
+            if (B == 13) RUNW(SmallProbe<13>, "small 2^13 + HotProbe, warm", true);
+            if (B == 14) RUNW(SmallProbe<14>, "small 2^14 + HotProbe, warm", true);
+        }
+        RUNW(HotProbe, "HotProbe, warm table again", true);
+    }
     RUN(RegionProbe<0>, "no probe");
     RUN(RegionProbe<12>, "probe 32 KB region");
     RUN(RegionProbe<17>, "probe 1 MB region");
