@@ -382,6 +382,33 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
 // *p |= bits (one thread; the II_TEST_LB_TIMEOUT test knob)
 __global__ void k_set_bits(uint64_t* p, unsigned long long bits) { atomicOr((unsigned long long*)p, bits); }
 
+// Stable LSD radix sort of n u32 keys on bits [0, bits): *k / *k2 ping-pong,
+// on return *k holds the sorted keys (the owner's merged pairs when lexid and
+// id0 fit one u32, ii_import).
+static int run_sort32(ii_ctx* c, uint32_t** k, uint32_t** k2, uint64_t n, int bits, int* passes) {
+    *passes = 0;
+    if (n <= 1 || bits <= 0) return II_OK;
+    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
+    uint64_t* table = P_<uint64_t>(c->rtable);
+    uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kSortTile - 1) / kSortTile);
+    const uint64_t chunk = ((n + nch - 1) / nch + kSortTile - 1) / kSortTile * kSortTile;
+    nch = (n + chunk - 1) / chunk;
+    const int npass = (bits + kRadixBits - 1) / kRadixBits, db = (bits + npass - 1) / npass;
+    for (int shift = 0; shift < bits; shift += db) {
+        const int w = std::min(db, bits - shift);
+        const uint32_t dmask = (1u << w) - 1u;
+        k_radix_hist<uint32_t><<<(uint32_t)nch, kBlock, 0, c->st>>>(*k, n, chunk, shift, dmask, (uint32_t)nch, table);
+        CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, nullptr));
+        k_radix_scatter<false, kScatterThreads, kScatterItems, false, uint32_t>
+            <<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(*k, *k2, nullptr, nullptr, n, chunk, shift, w, (uint32_t)nch,
+                                                           table, nullptr, nullptr, nullptr, 0, 0u);
+        HIPCK(hipGetLastError());
+        std::swap(*k, *k2);
+        (*passes)++;
+    }
+    return II_OK;
+}
+
 // Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
 // W-bit key when the other W - m key bits and the F id bits fit a u32 and
 // leave two LSD passes of <= kRadixBits bits; 0 = not packable.
@@ -444,7 +471,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
     k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-        *k2, nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
+        *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
         F, (1u << L) - 1u);
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
@@ -1466,13 +1493,31 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     uint64_t* wrec = P_<uint64_t>(c->rec);
     uint64_t* r = P_<uint64_t>(c->rec2);
     uint64_t* r2 = P_<uint64_t>(c->rec);
+    // which merge runs (the ordered check and the measured crossover are below); the owner's sort
+    // takes u32 records lexid << F | id0 when both fit one u32
+    bool ordered = true;
+    uint64_t prev_hi1 = 0;
+    for (int s = 0; s < nparts && ordered; s++) {
+        if (hdr[8 * s + 2] == 0) continue;
+        const uint64_t lo1 = hdr[8 * s + 6], hi1 = hdr[8 * s + 7];
+        if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
+        prev_hi1 = hi1;
+    }
+    constexpr int kMergeIdsMaxParts = 4;
+    const bool id_sort = getenv("II_IMPORT_ID_SORT") != nullptr;
+    const bool merge = !id_sort && (ordered || nparts <= kMergeIdsMaxParts);
+    const int Fid = std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), Lw = std::max(1, bitlen(c->V - 1));
+    const bool sort32 = !merge && Lw + Fid <= 32 && !(id_sort && !strcmp(getenv("II_IMPORT_ID_SORT"), "64"));
     uint64_t wbase = 0, pbase = 0;
     for (int s = 0; s < nparts; s++) {
         const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
-        if (np)
-            k_import_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
-                (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64), np, wbase, wrec, P_<uint32_t>(c->remap),
-                r + pbase);
+        const uint64_t* src = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
+        const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
+        if (np && sort32)
+            k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
+                                                          reinterpret_cast<uint32_t*>(r2) + pbase, Fid);
+        else if (np)
+            k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
         wbase += nw;
         pbase += np;
     }
@@ -1485,22 +1530,15 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // with interleaved ranges (ii_partition's size-sorted shards) and at most
     // kMergeIdsMaxParts sources, k_merge_ids places every pair by binary
     // searches of the word's other runs; with more sources (G - 1 searches per
-    // pair) the owner sorts: LSD over the id bits, then the word bits.
-    // Measured per owner (tools/exchange_timing.py, 10 GB over G interleaved
-    // shards): G = 2 merge 2.21 / sort 5.25 ms, G = 4 2.16 / 3.30, G = 8
-    // 2.41 / 2.04.  II_IMPORT_ID_SORT=1 (test knob) always sorts.
+    // pair) the owner sorts — one LSD radix sort of u32 records lexid << F |
+    // id0 when they fit 32 bits, else LSD over the id bits, then the word bits
+    // of the u64 records.  Measured per owner (tools/exchange_timing.py, 10 GB
+    // over G interleaved shards): G = 2 merge 2.21 / u64 sort 5.25 ms, G = 4
+    // 2.16 / 3.30, G = 8 2.41 / 2.04.  II_IMPORT_ID_SORT=1 (test knob) always
+    // sorts, =64 in the u64 form.
     int p1 = 0, p2 = 0;
     c->n_sc = 0;
-    bool ordered = true;
-    uint64_t prev_hi1 = 0;
-    for (int s = 0; s < nparts && ordered; s++) {
-        if (hdr[8 * s + 2] == 0) continue;
-        const uint64_t lo1 = hdr[8 * s + 6], hi1 = hdr[8 * s + 7];
-        if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
-        prev_hi1 = hi1;
-    }
-    constexpr int kMergeIdsMaxParts = 4;
-    if (!getenv("II_IMPORT_ID_SORT") && (ordered || nparts <= kMergeIdsMaxParts)) {
+    if (merge) {
         const uint64_t nk = c->V * (uint64_t)nparts;
         CK(grow(c->mstart, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
         CK(grow(c->mend, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
@@ -1536,10 +1574,15 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         }
         HIPCK(hipGetLastError());
         std::swap(r, r2);
+    } else if (sort32) {  // r2 holds the u32 records (its second half is the ping-pong buffer)
+        uint32_t* a = reinterpret_cast<uint32_t*>(r2);
+        uint32_t* b = a + NP;
+        CK(run_sort32(c, &a, &b, NP, Lw + Fid, &p1));
+        k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, r);
+        HIPCK(hipGetLastError());
     } else {
-        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), false,
-                    &p1));
-        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + std::max(1, bitlen(c->V - 1)), true, &p2));
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, Fid, false, &p1));
+        CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + Lw, true, &p2));
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;

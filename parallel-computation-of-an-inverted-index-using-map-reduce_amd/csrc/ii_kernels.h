@@ -818,21 +818,29 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
 
 // The fast path's hot-table probe (K1b step 3): the slot of a token's word
 // from the two 16-B slot pairs that begin its probe order, kSlotNone when the
-// word is left to K1c.  The home slot's pair first; only a lane whose home pair
-// is full without its key loads the next pair: the vector L1 handles a probe
-// lane by lane (random lines), so the lanes left out of an instruction are
-// what it saves.  (A policy type: tools/k1_ablate.hip times the same kernel
-// body with other probes, e.g. none.)
+// word is left to K1c.  The home slot's pair first (begin: its load is issued,
+// and K1b builds the next batch's keys while it is in flight); only a lane
+// whose home pair is full without its key loads the next pair (finish): the
+// vector L1 handles a probe lane by lane (random lines), so the lanes left out
+// of an instruction are what it saves.  (A policy type: tools/k1_ablate.hip
+// times the same kernel body with other probes, e.g. none.)
+struct ProbeState {
+    ulonglong2 qa;
+    uint32_t home;
+};
 struct HotProbe {
-    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
-                                                   uint64_t pos) const {
-        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
-        ulonglong2 qa = make_ulonglong2(1ull, 1ull), qb = make_ulonglong2(1ull, 1ull);
-        if (fast) qa = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + start);
-        uint32_t match = (uint32_t)(qa.x == key) | ((uint32_t)(qa.y == key) << 1);
-        uint32_t empty = (uint32_t)(qa.x == 0ull) | ((uint32_t)(qa.y == 0ull) << 1);
+    __device__ __forceinline__ ProbeState begin(const Table& t, bool fast, uint64_t key, uint32_t home) const {
+        ProbeState st{make_ulonglong2(1ull, 1ull), home};
+        if (fast) st.qa = *reinterpret_cast<const ulonglong2*>(t.keys + (home & ~1u));
+        return st;
+    }
+    __device__ __forceinline__ uint32_t finish(const Table& t, const ProbeState& st, bool fast, uint64_t key,
+                                              uint64_t pos) const {
+        const uint32_t bbase = st.home & ~(uint32_t)(kBucket - 1), start = st.home & (kBucket - 2);
+        uint32_t match = (uint32_t)(st.qa.x == key) | ((uint32_t)(st.qa.y == key) << 1);
+        uint32_t empty = (uint32_t)(st.qa.x == 0ull) | ((uint32_t)(st.qa.y == 0ull) << 1);
         if (fast && !(match | empty)) {
-            qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
+            const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
             match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
             empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
         }
@@ -907,17 +915,29 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
         }
         wave_sync();
         const uint32_t pbase = (uint32_t)(lo - chunk_lo);
-        // 3. keys + cooperative hot-bucket probes, one token per lane (issuing
-        //    the next batch's probes before resolving this one measured slower:
-        //    13.4 -> 14.6 ms at 10 GB, the extra registers cost a wave per SIMD)
+        // 3. keys + hot-bucket probes, one token per lane, 64 tokens a batch; the
+        //    next batch's keys are built (LDS + VALU) while this batch's probe
+        //    load is in flight.  (Issuing the next batch's PROBES before
+        //    resolving this one measured slower: 13.4 -> 14.6 ms at 10 GB, the
+        //    extra registers cost a wave per SIMD.)
+        uint32_t p_n = l < ntok ? W.off[l] : 0u;
+        TokKey tk_n{0ull, 0u, 0u};
+        bool fast_n = l < ntok && round_fast_key(W.text, W.mask, p_n, tk_n);
         for (uint32_t b0 = 0; b0 < ntok; b0 += 64) {
             const uint32_t q = b0 + l;
             const bool valid = q < ntok;
-            const uint32_t p = valid ? W.off[q] : 0u;
-            TokKey tk{0ull, 0u, 0u};
-            const bool fast = valid && round_fast_key(W.text, W.mask, p, tk);
+            const uint32_t p = p_n;
+            const TokKey tk = tk_n;
+            const bool fast = fast_n;
             if (fast) atomicAdd(&W.hist[tk.first], 1u);  // LDS: same-letter lanes serialize in the LDS unit, not in VALU
-            const uint32_t slot = Probe()(tab, fast, tk.key, hot_slot(tk.key, tab.seed), lo + p);
+            const ProbeState pst = Probe().begin(tab, fast, tk.key, hot_slot(tk.key, tab.seed));
+            if (b0 + 64 < ntok) {  // (wave-uniform) the next batch's keys
+                const uint32_t qn = q + 64;
+                p_n = qn < ntok ? W.off[qn] : 0u;
+                tk_n = TokKey{0ull, 0u, 0u};
+                fast_n = qn < ntok && round_fast_key(W.text, W.mask, p_n, tk_n);
+            }
+            const uint32_t slot = Probe().finish(tab, pst, fast, tk.key, lo + p);
             const bool resolved = fast && slot != kSlotNone;
             bool pf = fast && !resolved, ps = valid && !fast;
             uint64_t mf = __ballot(pf);
@@ -2094,14 +2114,27 @@ __global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint6
 }
 
 // received pair -> (global lexid, id0): word k of the merged word text was
-// tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id
+// tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id.
+// k32: the u32 record lexid << f32 | id0 instead (the owner's sort keys fit 32 bits)
+template <bool k32>
 __global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restrict__ pairs, uint64_t np, uint64_t wbase,
                                                          const uint64_t* __restrict__ wrec,
-                                                         const uint32_t* __restrict__ remap, uint64_t* __restrict__ out) {
+                                                         const uint32_t* __restrict__ remap, void* __restrict__ out,
+                                                         int f32) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
         uint64_t r = pairs[i];
         uint64_t slot = wrec[wbase + (r >> 32)] >> 32;
-        out[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
+        if (k32) static_cast<uint32_t*>(out)[i] = (remap[slot] << f32) | (uint32_t)r;
+        else static_cast<uint64_t*>(out)[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
+    }
+}
+// u32 records lexid << f | id0 -> the u64 records lexid << 32 | id0 K3 reads
+__global__ __launch_bounds__(kBlock) void k_unpack32(const uint32_t* __restrict__ in, uint64_t n, int f,
+                                                     uint64_t* __restrict__ out) {
+    const uint32_t m = (1u << f) - 1u;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t x = in[i];
+        out[i] = ((uint64_t)(x >> f) << 32) | (x & m);
     }
 }
 

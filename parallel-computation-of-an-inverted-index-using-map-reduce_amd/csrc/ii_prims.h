@@ -161,8 +161,9 @@ constexpr int kSweepTile = kSweepThreads * kSweepItems;  // keys per onesweep ti
 
 // Per-chunk digit histogram -> table[digit * nchunks + chunk] (digit-major, so
 // one exclusive scan of the table yields every chunk's scatter base).  Same
-// tile grid and item mapping as the scatter.
-__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, uint64_t chunk,
+// tile grid and item mapping as the scatter.  K: u64 or u32 keys.
+template <class K = uint64_t>
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const K* __restrict__ keys, uint64_t n, uint64_t chunk,
                                                        int shift, uint32_t dmask, uint32_t nchunks,
                                                        uint64_t* __restrict__ table) {
     __shared__ uint32_t cnt[kWaves][kRadix];
@@ -170,24 +171,32 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint32_t* mine = cnt[wave_id()];
-    // the histogram ignores order: 16-B loads (two keys per lane, 1 KiB per
-    // wave instruction); lo and the tile are even, so a pair is split only at hi
-    const uint64_t pofs = (uint64_t)wave_id() * 64 * kSortItems + 2 * (uint64_t)lane_id();
+    // the histogram ignores order: 16-B loads (kv keys per lane, 1 KiB per wave
+    // instruction); lo and the tile are multiples of kv, so a load is split only at hi
+    constexpr int kv = 16 / (int)sizeof(K);
+    const uint64_t pofs = (uint64_t)wave_id() * 64 * kSortItems + kv * (uint64_t)lane_id();
     for (uint64_t tb = lo; tb < hi; tb += kSortTile) {
-        ulonglong2 raw[kSortItems / 2];
+        K raw[kSortItems];
 #pragma unroll
-        for (int k = 0; k < kSortItems / 2; k++) {
-            const uint64_t idx = tb + pofs + (uint64_t)k * 128;
-            if (idx + 1 < hi) {
+        for (int k = 0; k < kSortItems / kv; k++) {
+            const uint64_t idx = tb + pofs + (uint64_t)k * 64 * kv;
+            if (idx + kv - 1 < hi) {
                 const uint4 v = ld_nt16(keys + idx);
-                raw[k] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32));
-            } else raw[k] = make_ulonglong2(idx < hi ? keys[idx] : 0ull, 0ull);
+                if constexpr (sizeof(K) == 8) {
+                    raw[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                    raw[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+                } else {
+                    raw[4 * k] = v.x; raw[4 * k + 1] = v.y; raw[4 * k + 2] = v.z; raw[4 * k + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kv; u++) raw[kv * k + u] = idx + u < hi ? keys[idx + u] : (K)0;
+            }
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems / 2; k++) {
-            const uint64_t idx = tb + pofs + (uint64_t)k * 128;
-            if (idx < hi) atomicAdd(&mine[(uint32_t)(raw[k].x >> shift) & dmask], 1u);
-            if (idx + 1 < hi) atomicAdd(&mine[(uint32_t)(raw[k].y >> shift) & dmask], 1u);
+        for (int k = 0; k < kSortItems; k++) {
+            const uint64_t idx = tb + pofs + (uint64_t)(k / kv) * 64 * kv + k % kv;
+            if (idx < hi) atomicAdd(&mine[(uint32_t)(raw[k] >> shift) & dmask], 1u);
         }
     }
     __syncthreads();
@@ -215,8 +224,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t* __restric
 // record (key << 32 | id) goes out as the u32 (key & pack_low) << pack_f | id
 // — the digit (the key's top bits) is implied by the bucket it lands in — and
 // digit d's output starts pad[d] records later (buckets padded to whole tiles).
-template <bool kHasVals, int NT = kBlock, int IT = kSortItems, bool kPack = false>
-__global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+template <bool kHasVals, int NT = kBlock, int IT = kSortItems, bool kPack = false, class K = uint64_t>
+__global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin, K* __restrict__ kout,
                                                       const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
                                                       uint64_t n, uint64_t chunk, int shift, int dbits,
                                                       uint32_t nchunks, const uint64_t* __restrict__ table,
@@ -226,7 +235,8 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
     constexpr int kTileN = NT * IT;
     constexpr int kDW = kRadix / 64;  // waves that own digits
     static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
-    __shared__ uint64_t s_keys[kTileN];
+    static_assert(!kPack || sizeof(K) == 8, "the packed MSD scatter reads u64 records");
+    __shared__ K s_keys[kTileN];
     __shared__ uint32_t s_vals[kHasVals ? kTileN : 1];
     __shared__ uint32_t s_wcnt[NW][kRadix];
     __shared__ uint32_t s_tstart[kRadix];
@@ -242,14 +252,14 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
     const uint64_t lt = lanemask_lt();
 
     // the next tile's keys are loaded while this tile is ranked and written
-    uint64_t nkey[IT];
+    K nkey[IT];
     uint32_t nval[IT];
     auto load_tile = [&](uint64_t tb) {
         const uint64_t wb = tb + (uint64_t)w * 64 * IT + l;
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const uint64_t idx = wb + (uint64_t)k * 64;
-            nkey[k] = idx < hi ? kin[idx] : ~0ull;
+            nkey[k] = idx < hi ? kin[idx] : (K)~0ull;
             if (kHasVals) nval[k] = idx < hi ? vin[idx] : 0u;
         }
     };
@@ -260,7 +270,7 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
 #pragma unroll
             for (int ww = 0; ww < NW; ww++) s_wcnt[ww][t] = 0;
         }
-        uint64_t key[IT];
+        K key[IT];
         uint32_t val[IT];
         uint32_t rank[IT];
         const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
@@ -341,10 +351,10 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const uint64_t* __restrict
         for (int j = 0; j < IT; j++) {
             const uint32_t p = j * NT + t;
             if (p < tile_n) {
-                const uint64_t k = s_keys[p];
+                const K k = s_keys[p];
                 const uint32_t d = (uint32_t)(k >> shift) & dmask;
                 const uint64_t dst = s_run[d] + (p - s_tstart[d]);
-                if (kPack) kout32[dst] = (((uint32_t)(k >> 32) & pack_low) << pack_f) | (uint32_t)k;
+                if constexpr (kPack) kout32[dst] = (((uint32_t)((uint64_t)k >> 32) & pack_low) << pack_f) | (uint32_t)k;
                 else kout[dst] = k;
                 if (kHasVals) vout[dst] = s_vals[p];
             }

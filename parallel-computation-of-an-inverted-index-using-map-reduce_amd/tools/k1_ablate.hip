@@ -51,36 +51,20 @@ float best_of(F f) {
 }
 
 // probe of the same shape as HotProbe's first load, confined to 2^B slots; the slot is the home slot
+// (B = 0: no load at all)
 template <int B>
 struct RegionProbe {
-    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home, uint64_t) const {
+    __device__ __forceinline__ ProbeState begin(const Table& t, bool fast, uint64_t, uint32_t home) const {
+        ProbeState st{make_ulonglong2(0ull, 0ull), home};
+        if (B && fast) st.qa = *reinterpret_cast<const ulonglong2*>(t.keys + (home & ((1u << (B ? B : 1)) - 2u)));
+        return st;
+    }
+    __device__ __forceinline__ uint32_t finish(const Table&, const ProbeState& st, bool fast, uint64_t key,
+                                              uint64_t) const {
         if (!fast) return kSlotNone;
-        if (B == 0) return home;
-        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(t.keys + (home & ((1u << B) - 2u)));
-        return q.x == key + 1 ? kSlotNone : home;  // (never equal in practice: keeps the load)
+        return st.qa.x == key + 1 ? kSlotNone : st.home;  // (never equal in practice: keeps the load)
     }
 };
-// HotProbe with the bucket's first NP slot pairs (in probe order) loaded at once: one round trip
-template <int NP>
-struct WideProbe {
-    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
-                                                   uint64_t pos) const {
-        if (!fast) return kSlotNone;
-        const uint32_t bbase = home & ~(uint32_t)(kBucket - 1), start = home & (kBucket - 2);
-        ulonglong2 q[NP];
-#pragma unroll
-        for (int j = 0; j < NP; j++)
-            q[j] = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2 * j) & (kBucket - 2)));
-        uint32_t match = 0, empty = 0;
-#pragma unroll
-        for (int j = 0; j < NP; j++) {
-            match |= ((uint32_t)(q[j].x == key) << (2 * j)) | ((uint32_t)(q[j].y == key) << (2 * j + 1));
-            empty |= ((uint32_t)(q[j].x == 0ull) << (2 * j)) | ((uint32_t)(q[j].y == 0ull) << (2 * j + 1));
-        }
-        return bucket_resolve(t, match, empty, key, bbase, start, pos);
-    }
-};
-
 // A small direct-mapped cache in front of HotProbe: (key, slot) of the most frequent hot words
 // (found by counting a previous run's records, tools only), 2^B entries of 16 B; a miss takes HotProbe.
 // What a sampling pre-pass could buy: the share of tokens served by an L1 / L2-resident table.
@@ -91,12 +75,16 @@ __host__ __device__ __forceinline__ uint32_t small_hash(uint64_t key) {
 }
 template <int B>
 struct SmallProbe {
-    __device__ __forceinline__ uint32_t operator()(const Table& t, bool fast, uint64_t key, uint32_t home,
-                                                   uint64_t pos) const {
-        ulonglong2 e = make_ulonglong2(0ull, 0ull);
-        if (fast) e = g_small[small_hash(key) & ((1u << B) - 1u)];
-        if (fast && e.x == key) return (uint32_t)e.y;
-        return HotProbe()(t, fast && e.x != key, key, home, pos);
+    __device__ __forceinline__ ProbeState begin(const Table& t, bool fast, uint64_t key, uint32_t home) const {
+        ProbeState st{make_ulonglong2(0ull, 0ull), home};
+        if (fast) st.qa = g_small[small_hash(key) & ((1u << B) - 1u)];
+        return st;
+    }
+    __device__ __forceinline__ uint32_t finish(const Table& t, const ProbeState& st, bool fast, uint64_t key,
+                                              uint64_t pos) const {
+        if (fast && st.qa.x == key) return (uint32_t)st.qa.y;
+        const bool miss = fast && st.qa.x != key;
+        return HotProbe().finish(t, HotProbe().begin(t, miss, key, st.home), miss, key, pos);
     }
 };
 
@@ -187,7 +175,6 @@ int main(int argc, char** argv) {
 #define RUN(A, name) RUNW(A, name, false)
     printf("bytes %llu tokens %llu count %.3f ms\n", (unsigned long long)nb, (unsigned long long)T, ms_count);
     RUN(HotProbe, "full (HotProbe)");
-    RUN(WideProbe<2>, "two pairs at once");
     // small front tables of the most frequent hot words (counted from the records of a warm run)
     RUNW(HotProbe, "HotProbe, warm table", true);
     {
