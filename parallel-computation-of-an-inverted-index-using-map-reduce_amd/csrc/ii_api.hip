@@ -35,6 +35,11 @@ constexpr int kMaxTimedPasses = 16;
 struct ii_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
+    hipStream_t st2 = nullptr;  // side stream: the exactness check of hashed keys (k_long_verify) beside the reduce
+    bool lv_pending = false;    // a k_long_verify on st2 whose verdict the host has not read yet (ev_res[1])
+    bool test_collide = false;  // test knob II_TEST_COLLIDE=1: the first check of the context reports a collision
+    uint32_t collide_retries = 0;
+    uint64_t* hbuf = nullptr;   // pinned host words for readbacks queued before a later sync
 
     // input
     DBuf text_own;  // text copied in by ii_map_host / ii_map_files
@@ -599,17 +604,20 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     c->dev = device;
     HIPCK(hipSetDevice(device));
     HIPCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HIPCK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_c0) HIPCK(hipEventCreate(&e));
+    HIPCK(hipHostMalloc((void**)&c->hbuf, 64 * sizeof(uint64_t), hipHostMallocDefault));
     if (grow(c->partial, sizeof(uint64_t) * (2 * kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
         return II_ERR_NOMEM;
     }
     c->test_lb_timeout = getenv("II_TEST_LB_TIMEOUT") && !strcmp(getenv("II_TEST_LB_TIMEOUT"), "1");
+    c->test_collide = getenv("II_TEST_COLLIDE") && !strcmp(getenv("II_TEST_COLLIDE"), "1");
     const char* s = getenv("II_TABLE_LOG2");
     if (s && atoi(s) >= 10 && atoi(s) <= 30) c->big_cap = 1ull << atoi(s);
     memset(&c->stats, 0, sizeof(c->stats));
@@ -643,6 +651,9 @@ extern "C" void ii_close(ii_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_c0)
         if (e) (void)hipEventDestroy(e);
+    if (c->st2) (void)hipStreamSynchronize(c->st2);
+    if (c->st2) (void)hipStreamDestroy(c->st2);
+    if (c->hbuf) (void)hipHostFree(c->hbuf);
     for (auto s : c->io_st) (void)hipStreamSynchronize(s);
     for (auto s : c->io_st) (void)hipStreamDestroy(s);
     for (auto e : c->io_ev) (void)hipEventDestroy(e);
@@ -693,8 +704,16 @@ static uint32_t narrow_keys() {
     return v < kNarrowKeys ? (uint32_t)v : (uint32_t)kNarrowKeys;
 }
 
-// dense: records of token k at rec[k] (the import path indexes them so)
+// dense: records of token k at rec[k] (the import path indexes them so).
+// The main map (not dense) leaves the exactness check of its hashed keys
+// (k_long_verify) running on the side stream while the reduce proceeds on the
+// main one; local_reduce reads its verdict after K3 (check_long_words) and
+// re-runs map + reduce with a new seed on a collision.  The import's word
+// map checks at once.
 static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = false) {
+    // a check of an earlier map still reads the table, the long queue and the counters
+    if (c->lv_pending) HIPCK(hipStreamWaitEvent(c->st, c->ev_res[1], 0));
+    c->lv_pending = false;
     c->mapped = c->have_pairs = c->reduced = false;
     c->wid_pairs = false;
     c->planned_parts = 0;
@@ -778,11 +797,12 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
         HIPCK(hipGetLastError());
         CK(run_reduce(c, OpOccupied{P_<unsigned long long>(c->tkeys)}, nslots, counters + C_INSERT));
-        HIPCK(hipEventRecord(c->ev_res[0], c->st));
-        k_long_verify<<<dim3(kLongShards, kLvBlocks), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<LongTok>(c->longs),
-                                                                         c->long_cap / kLongShards,
-                                                                         P_<uint64_t>(c->trep), counters);
-        HIPCK(hipEventRecord(c->ev_res[1], c->st));
+        if (dense) {
+            HIPCK(hipEventRecord(c->ev_res[0], c->st));
+            k_long_verify<<<dim3(kLongShards, kLvBlocks), kBlock, 0, c->st>>>(
+                c->text, c->nbytes, P_<LongTok>(c->longs), c->long_cap / kLongShards, P_<uint64_t>(c->trep), counters);
+            HIPCK(hipEventRecord(c->ev_res[1], c->st));
+        }
         if (c->rec_cap) CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));  // chunk token counts -> voff
         k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
         HIPCK(hipGetLastError());
@@ -817,6 +837,18 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     }
     if (hist_out) memcpy(hist_out, c->hist, sizeof(c->hist));
     HIPCK(hipEventRecord(c->ev[1], c->st));
+    if (!dense) {  // the exactness check on the side stream, after K1b (ev[1])
+        uint64_t* counters_d = P_<uint64_t>(c->counters);
+        HIPCK(hipStreamWaitEvent(c->st2, c->ev[1], 0));
+        HIPCK(hipEventRecord(c->ev_res[0], c->st2));
+        k_long_verify<<<dim3(kLongShards, kLvBlocks), kBlock, 0, c->st2>>>(
+            c->text, c->nbytes, P_<LongTok>(c->longs), c->long_cap / kLongShards, P_<uint64_t>(c->trep), counters_d);
+        if (c->test_collide) k_set_bits<<<1, 1, 0, c->st2>>>(counters_d + C_COLLIDE, 1ull);
+        c->test_collide = false;
+        HIPCK(hipEventRecord(c->ev_res[1], c->st2));
+        HIPCK(hipGetLastError());
+        c->lv_pending = true;
+    }
     c->mapped = true;
     return II_OK;
 }
@@ -844,6 +876,7 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
     c->h_fid.assign(file_id0, file_id0 + nfiles);
     c->part_valid = false;
     c->text_is_input = true;
+    c->collide_retries = 0;
     return II_OK;
 }
 
@@ -1235,8 +1268,27 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
         if (ovf & kLbTimeout) return II_ERR_INTERNAL;  // a onesweep look-back never resolved
     }
 
-    // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts
+    // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts.  The verdict of
+    // the map's exactness check (k_long_verify on the side stream, map_core) is read with K3's
+    // results (one host round trip); two long words with one hashed key: new seed, map + reduce again
+    const bool check = c->lv_pending;
+    if (check) {
+        HIPCK(hipStreamWaitEvent(c->st, c->ev_res[1], 0));
+        HIPCK(hipMemcpyAsync(c->hbuf, P_<uint64_t>(c->counters) + C_COLLIDE, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             c->st));
+    }
     CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_ident ? nullptr : P_<uint32_t>(c->fid)));
+    if (check) {
+        c->lv_pending = false;
+        if (c->hbuf[0]) {  // (Las Vegas: the output never depends on the seed)
+            if (++c->collide_retries > 12) return II_ERR_INTERNAL;
+            c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
+            const uint32_t r0 = c->retries;
+            CK(map_core(c, nullptr));
+            c->retries += r0 + 1;
+            return local_reduce(c, wid);
+        }
+    }
     c->wid_pairs = wid;
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)sort_passes;

@@ -479,3 +479,21 @@ def test_k3_lookback_timeout_is_an_error():
             assert e.value.code == -7
     finally:
         os.environ.pop("II_TEST_LB_TIMEOUT", None)
+
+
+def test_long_word_collision_retry():
+    """The exactness check of hashed (> 12-letter) keys runs on a side stream
+    beside the reduce; its verdict is read with K3's results, and a collision
+    re-runs map + reduce with a new seed.  II_TEST_COLLIDE=1 makes the first
+    check of a context report one: same output, one more retry."""
+    text, off, ids = long_variant_corpus(33)
+    exp = oracle_index(text, off, ids)
+    os.environ["II_TEST_COLLIDE"] = "1"
+    try:
+        with ii_ctypes.Index(0) as ix:
+            ix.map_host(text, off, ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, "collision retry")
+            assert ix.stats().retries >= 1
+    finally:
+        os.environ.pop("II_TEST_COLLIDE", None)
