@@ -54,6 +54,7 @@ struct ii_ctx {
 
     // scratch
     DBuf partial, totals, counters, chunk_cnt, chunk_hist, rtable, kept;
+    DBuf partial2, rtable2, kept2;  // the same scratch for work queued on st2 (SideScope)
     // K1
     DBuf rec, rec2, longs, pend, pend_cnt, chunk_files;
     DBuf tkeys, trep;
@@ -109,6 +110,7 @@ struct ii_ctx {
     int n_sc = 0;
     uint64_t T_sorted = 0;  // records left after the pass-0 dedup
     hipEvent_t ev_c0[2] = {};  // around k_sort0_compact
+    hipEvent_t ev_dict[2] = {};  // the dictionary's lexicographic part on st2: may start / done
     uint64_t c0_bytes = 0;     // its algorithmic bytes (records read + kept records written)
     bool sort_packed = false;  // the last token sort ran in the packed form (run_sort_packed)
     int sort_W = 0, sort_F = 0;  // its key / file-index bits
@@ -610,8 +612,10 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_c0) HIPCK(hipEventCreate(&e));
+    for (auto& e : c->ev_dict) HIPCK(hipEventCreate(&e));
     HIPCK(hipHostMalloc((void**)&c->hbuf, 64 * sizeof(uint64_t), hipHostMallocDefault));
-    if (grow(c->partial, sizeof(uint64_t) * (2 * kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
+    if (grow(c->partial, sizeof(uint64_t) * (2 * kMaxChunks + 1)) ||
+        grow(c->partial2, sizeof(uint64_t) * (2 * kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
         return II_ERR_NOMEM;
@@ -629,6 +633,7 @@ extern "C" void ii_close(ii_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->st2) (void)hipStreamSynchronize(c->st2);  // (work on st2 reads the buffers freed below)
     DBuf* all[] = {&c->text_own, &c->fstart, &c->fid,   &c->partial, &c->totals, &c->counters, &c->chunk_cnt, &c->chunk_hist,
                    &c->rtable,   &c->rec,    &c->rec2,  &c->longs,   &c->tkeys,  &c->trep,     &c->dslot,
                    &c->dkey,     &c->dkey2,  &c->didx,  &c->didx2,   &c->remap,  &c->lkey,     &c->lrep,
@@ -638,7 +643,8 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
-                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk, &c->moff};
+                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk, &c->moff,
+                   &c->partial2, &c->rtable2, &c->kept2};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -650,6 +656,8 @@ extern "C" void ii_close(ii_ctx* c) {
     for (auto& e : c->ev_res)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_c0)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_dict)
         if (e) (void)hipEventDestroy(e);
     if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->st2) (void)hipStreamDestroy(c->st2);
@@ -1126,8 +1134,27 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
 }
 
 // ----------------------------------------------------------------- reduce
-static int build_dictionary(ii_ctx* c, bool wid = false) {
-    uint64_t* counters = P_<uint64_t>(c->counters);
+// Work queued on the side stream st2 with scratch of its own: run_sort and
+// run_scan take c->st, c->rtable, c->partial and c->kept, so for the life of
+// the object those name st2's copies.  (A host-side swap: kernels capture
+// their pointers at launch, so work queued earlier keeps its buffers.)
+struct SideScope {
+    ii_ctx* c;
+    explicit SideScope(ii_ctx* c_) : c(c_) { swap(); }
+    ~SideScope() { swap(); }
+    void swap() {
+        std::swap(c->st, c->st2);
+        std::swap(c->partial, c->partial2);
+        std::swap(c->rtable, c->rtable2);
+        std::swap(c->kept, c->kept2);
+    }
+};
+
+// Dictionary, part 1 — all the token sort needs: every dictionary buffer
+// grown, the occupied slots compacted (dslot, ascending: V of them; the count
+// is copied to hbuf[1] for a check after a later synchronisation) and, for
+// word-id keys, the hot-slot count and the big-table words' ids (wmap).
+static int dict_slots(ii_ctx* c, bool wid) {
     uint64_t* totals = P_<uint64_t>(c->totals);
     const uint32_t V = (uint32_t)c->V;
     CK(grow(c->dslot, sizeof(uint32_t) * (V + 1)));
@@ -1142,15 +1169,35 @@ static int build_dictionary(ii_ctx* c, bool wid = false) {
     CK(grow(c->llen, sizeof(uint32_t) * (V + 1)));
     CK(grow(c->lstart, sizeof(uint32_t) * (II_ALPHABET + 1)));
     CK(grow(c->tied, sizeof(uint32_t) * (V + 1)));
+    CK(grow(c->rtable2, sizeof(uint64_t) * kRadix * kMaxChunks));  // st2's sort scratch, grown here (never
+    CK(grow(c->kept2, sizeof(uint64_t) * 2 * kMaxChunks));           // reallocated while st2 runs)
+    uint32_t* dslot = P_<uint32_t>(c->dslot);
+    CK(run_scan(c, OpCompactSlots{P_<unsigned long long>(c->tkeys), dslot}, nslots, totals + 1));
+    HIPCK(hipMemcpyAsync(c->hbuf + 1, totals + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    if (wid) {  // word ids of the single-GPU token sort (k_wid_map; k_wid_finish after the lexicographic sort)
+        CK(grow(c->wmap, sizeof(uint32_t) * nslots));
+        CK(grow(c->lexw, sizeof(uint32_t) * (kHotSlots + V)));
+        CK(grow(c->widl, sizeof(uint32_t) * (V + 1)));
+        uint32_t* nhot = reinterpret_cast<uint32_t*>(totals + 7);
+        HIPCK(hipMemsetAsync(totals + 7, 0, sizeof(uint64_t), c->st));
+        k_count_hot<<<grid_for(V), kBlock, 0, c->st>>>(dslot, V, nhot);
+        k_wid_map<<<grid_for(V), kBlock, 0, c->st>>>(dslot, V, nhot, P_<uint32_t>(c->wmap));
+        HIPCK(hipGetLastError());
+        c->NW = kHotSlots + V;  // bound; run_sort refines it from totals[7] after its first pass (no extra sync)
+    }
+    return II_OK;
+}
 
+// Dictionary, part 2: the lexicographic order of the V words (prefix-key
+// sort, ties of longer words), remap / lkey / lrep / llen / lstart, and for
+// word-id keys wid <-> lexid (lexw, widl).  Needs dict_slots' results.
+static int dict_lex(ii_ctx* c, bool wid) {
+    uint64_t* counters = P_<uint64_t>(c->counters);
+    uint64_t* totals = P_<uint64_t>(c->totals);
+    const uint32_t V = (uint32_t)c->V;
     const unsigned long long* keys = P_<unsigned long long>(c->tkeys);
     const uint64_t* rep = P_<uint64_t>(c->trep);
     uint32_t* dslot = P_<uint32_t>(c->dslot);
-    CK(run_scan(c, OpCompactSlots{keys, dslot}, nslots, totals + 1));
-    uint64_t vchk;
-    CK(read_u64(c, totals + 1, &vchk));
-    if (vchk != V) return II_ERR_INTERNAL;
-
     uint64_t* sk = P_<uint64_t>(c->dkey);
     uint64_t* sk2 = P_<uint64_t>(c->dkey2);
     uint32_t* di = P_<uint32_t>(c->didx);
@@ -1202,22 +1249,22 @@ static int build_dictionary(ii_ctx* c, bool wid = false) {
     k_lex_finish<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, di, dslot, keys, rep, V, P_<uint32_t>(c->remap),
                                                    P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen));
     k_letter_start<<<grid_for(V + 1), kBlock, 0, c->st>>>(sk, V, P_<uint32_t>(c->lstart));
-    HIPCK(hipGetLastError());
-    if (wid) {  // word ids of the single-GPU token sort (k_wid_finish)
-        CK(grow(c->wmap, sizeof(uint32_t) * nslots));
-        CK(grow(c->lexw, sizeof(uint32_t) * (kHotSlots + V)));
-        CK(grow(c->widl, sizeof(uint32_t) * (V + 1)));
-        uint32_t* nhot = reinterpret_cast<uint32_t*>(totals + 7);
-        HIPCK(hipMemsetAsync(totals + 7, 0, sizeof(uint64_t), c->st));
-        k_count_hot<<<grid_for(V), kBlock, 0, c->st>>>(dslot, V, nhot);
-        k_wid_finish<<<grid_for(V), kBlock, 0, c->st>>>(di, dslot, V, nhot, P_<uint32_t>(c->wmap),
+    if (wid)
+        k_wid_finish<<<grid_for(V), kBlock, 0, c->st>>>(di, dslot, V, reinterpret_cast<const uint32_t*>(totals + 7),
                                                        P_<uint32_t>(c->lexw), P_<uint32_t>(c->widl));
-        HIPCK(hipGetLastError());
-        c->NW = kHotSlots + V;  // bound; run_sort refines it from totals[7] after its first pass (no extra sync)
-    }
+    HIPCK(hipGetLastError());
     // keep the sorted prefix keys in dkey for the order step
     if (sk != P_<uint64_t>(c->dkey)) std::swap(c->dkey, c->dkey2);
     return II_OK;
+}
+
+// The whole dictionary in stream order (the owner's import; lexid-keyed sorts).
+static int build_dictionary(ii_ctx* c, bool wid = false) {
+    CK(dict_slots(c, wid));
+    uint64_t vchk;
+    CK(read_u64(c, P_<uint64_t>(c->totals) + 1, &vchk));
+    if (vchk != c->V) return II_ERR_INTERNAL;
+    return dict_lex(c, wid);
 }
 
 // Local reduce: dictionary (lexicographic ids), K2 token sort, K3 unique
@@ -1239,7 +1286,16 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     }
     // ---- dictionary: lexicographic ids
     if (getenv("II_SORT_KEYS") && !strcmp(getenv("II_SORT_KEYS"), "lexid")) wid = false;
-    CK(build_dictionary(c, wid));
+    // word-id keys: the token sort needs only the slot part of the dictionary;
+    // its lexicographic part (a sort of the V prefix keys, ~0.5 ms of small
+    // launches and host round trips) runs on st2 beside the sort, queued once
+    // the sort is; K3's word-id -> lexid step waits for it
+    if (wid) {
+        CK(dict_slots(c, true));
+        HIPCK(hipEventRecord(c->ev_dict[0], c->st));
+    } else {
+        CK(build_dictionary(c, false));
+    }
     HIPCK(hipEventRecord(c->ev[2], c->st));
 
     // ---- K2: sort records by (lexid, fid); fid order is kept by stability
@@ -1262,6 +1318,17 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
+    if (wid) {
+        HIPCK(hipEventSynchronize(c->ev_dict[0]));  // (the sort's own synchronisation is past it already)
+        if (c->hbuf[1] != V) return II_ERR_INTERNAL;
+        {
+            SideScope side(c);  // c->st is st2 in here
+            HIPCK(hipStreamWaitEvent(c->st, c->ev_dict[0], 0));
+            CK(dict_lex(c, true));
+            HIPCK(hipEventRecord(c->ev_dict[1], c->st));
+        }
+        HIPCK(hipStreamWaitEvent(c->st, c->ev_dict[1], 0));
+    }
     {
         uint64_t ovf;
         CK(read_u64(c, P_<uint64_t>(c->counters) + C_OVERFLOW, &ovf));
@@ -1524,7 +1591,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         o += ab;
     }
     CK(grow(c->rec, sizeof(uint64_t) * std::max<uint64_t>({W, NP, 1})));
-    CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>({W, NP, 1})));
+    CK(grow(c->rec2, sizeof(uint64_t) * std::max<uint64_t>({W, NP, 1}) + 16));  // + the u32 form's alignment pad
     c->text = P_<uint8_t>(c->text_own);
     c->nbytes = A;
     const uint64_t fs0 = 0;
@@ -1560,6 +1627,9 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     const bool merge = !id_sort && (ordered || nparts <= kMergeIdsMaxParts);
     const int Fid = std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), Lw = std::max(1, bitlen(c->V - 1));
     const bool sort32 = !merge && Lw + Fid <= 32 && !(id_sort && !strcmp(getenv("II_IMPORT_ID_SORT"), "64"));
+    // The pairs go to r (rec2) in both forms: r2 is rec, which holds the word
+    // records wrec every source's pairs are mapped through (writing the u32
+    // records there overwrote word records later sources still read).
     uint64_t wbase = 0, pbase = 0;
     for (int s = 0; s < nparts; s++) {
         const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
@@ -1567,7 +1637,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
         if (np && sort32)
             k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
-                                                          reinterpret_cast<uint32_t*>(r2) + pbase, Fid);
+                                                          reinterpret_cast<uint32_t*>(r) + pbase, Fid);
         else if (np)
             k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
         wbase += nw;
@@ -1626,12 +1696,14 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         }
         HIPCK(hipGetLastError());
         std::swap(r, r2);
-    } else if (sort32) {  // r2 holds the u32 records (its second half is the ping-pong buffer)
-        uint32_t* a = reinterpret_cast<uint32_t*>(r2);
-        uint32_t* b = a + NP;
+    } else if (sort32) {  // r holds the u32 records (its second half is the ping-pong buffer)
+        uint32_t* a = reinterpret_cast<uint32_t*>(r);
+        uint32_t* b = a + ((NP + 3) & ~3ull);  // 16-B aligned: k_radix_hist reads 16 B at a time
         CK(run_sort32(c, &a, &b, NP, Lw + Fid, &p1));
-        k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, r);
+        // the word records are no longer read: the u64 records go to r2 (rec)
+        k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, r2);
         HIPCK(hipGetLastError());
+        std::swap(r, r2);
     } else {
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, Fid, false, &p1));
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + Lw, true, &p2));
