@@ -619,7 +619,9 @@ def main():
         sp = max(1, st.sort_passes)
         survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
         k3_read = (4 if st.sort_packed else 8) * Tk  # the packed form's K3 reads u32 records
-        impl_b = 8 * T + 8 * Tk + st.sort_bytes + k3_read + 8 * U + 8 * (V + U // 64) + 16 * V
+        # (the pairs: 4 B each when K3 wrote the compact form, plus the word key of every 64th)
+        pair_b = (4 * U + 4 * (U // 64)) if st.pair_bytes == 4 else 8 * U
+        impl_b = 8 * T + 8 * Tk + st.sort_bytes + k3_read + pair_b + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_gbs = impl_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         pmc_b = pmc_phase_bytes(traffic) if traffic else None

@@ -98,6 +98,7 @@ typedef struct {
     uint32_t sort_packed;  /* 1: the packed form (u32 records in buckets, ii_prims.h) ran */
     uint32_t sort_key_bits;  /* W: bits of the token sort's word keys */
     uint32_t sort_id_bits;   /* F: bits of the records' shard-local file indices (packed form: W + F - 32 <= 8) */
+    uint32_t pair_bytes;     /* bytes per distinct pair K3 wrote: 4 (compact, formatted only) or 8 (exportable) */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

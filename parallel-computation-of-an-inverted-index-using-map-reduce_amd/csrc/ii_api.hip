@@ -70,6 +70,8 @@ struct ii_ctx {
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
     DBuf moff;              // ii_import merge of interleaved sources: per (word, source) merged offset
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
+    DBuf drank, g64;        // compact pairs: hot slot -> dense word index; word key of every 64th pair
+    bool pairs32 = false;   // uniq holds compact u32 pairs (k_uniq_sweep uniq32): formatted, never exported
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
     DBuf msd;                    // packed token sort: bucket geometry, per-bucket digit counts and bases
@@ -533,8 +535,10 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
 // (post_start[V] = U).  Sets c->U.  fmap: id0 of every shard-local file index
 // the records carry (null: the records carry id0s).
-static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed, const uint32_t* fmap) {
+static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed, const uint32_t* fmap,
+                      bool compact) {
     c->xpairs = false;
+    c->pairs32 = compact;
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
     CK(grow(c->pstart, sizeof(uint64_t) * (c->V + 1)));
@@ -544,6 +548,14 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
     uint64_t* Pp = P_<uint64_t>(c->P);
     uint64_t* ps = P_<uint64_t>(c->pstart);
     uint64_t* totals = P_<uint64_t>(c->totals);
+    uint32_t* u32 = nullptr;
+    uint32_t* g64 = nullptr;
+    if (compact) {  // (file ids below 2^31: the top bit marks a word's first pair)
+        if (c->id_bound > kPairFirst) return II_ERR_ARG;
+        CK(grow(c->g64, sizeof(uint32_t) * (n / 64 + 2)));
+        u32 = P_<uint32_t>(c->uniq);
+        g64 = P_<uint32_t>(c->g64);
+    }
     if (n == 0) {
         HIPCK(hipMemsetAsync(ps + c->V, 0, sizeof(uint64_t), c->st));
         HIPCK(hipMemsetAsync(Pp, 0, sizeof(uint64_t), c->st));
@@ -567,14 +579,14 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap);
+            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
         k_uniq_sweep<false><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
             P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW,
-            fmap);
+            fmap, u32, g64);
         k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     }
     if (wid)
@@ -644,7 +656,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
                    &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk, &c->moff,
-                   &c->partial2, &c->rtable2, &c->kept2};
+                   &c->partial2, &c->rtable2, &c->kept2, &c->drank, &c->g64};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -1172,7 +1184,9 @@ static int dict_slots(ii_ctx* c, bool wid) {
     CK(grow(c->rtable2, sizeof(uint64_t) * kRadix * kMaxChunks));  // st2's sort scratch, grown here (never
     CK(grow(c->kept2, sizeof(uint64_t) * 2 * kMaxChunks));           // reallocated while st2 runs)
     uint32_t* dslot = P_<uint32_t>(c->dslot);
-    CK(run_scan(c, OpCompactSlots{P_<unsigned long long>(c->tkeys), dslot}, nslots, totals + 1));
+    if (wid) CK(grow(c->drank, sizeof(uint32_t) * kHotSlots));
+    CK(run_scan(c, OpCompactSlots{P_<unsigned long long>(c->tkeys), dslot, wid ? P_<uint32_t>(c->drank) : nullptr},
+                nslots, totals + 1));
     HIPCK(hipMemcpyAsync(c->hbuf + 1, totals + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
     if (wid) {  // word ids of the single-GPU token sort (k_wid_map; k_wid_finish after the lexicographic sort)
         CK(grow(c->wmap, sizeof(uint32_t) * nslots));
@@ -1253,8 +1267,10 @@ static int dict_lex(ii_ctx* c, bool wid) {
         k_wid_finish<<<grid_for(V), kBlock, 0, c->st>>>(di, dslot, V, reinterpret_cast<const uint32_t*>(totals + 7),
                                                        P_<uint32_t>(c->lexw), P_<uint32_t>(c->widl));
     HIPCK(hipGetLastError());
-    // keep the sorted prefix keys in dkey for the order step
+    // keep the sorted prefix keys in dkey for the order step, their dictionary
+    // indices in didx (the compact pairs' formatter)
     if (sk != P_<uint64_t>(c->dkey)) std::swap(c->dkey, c->dkey2);
+    if (di != P_<uint32_t>(c->didx)) std::swap(c->didx, c->didx2);
     return II_OK;
 }
 
@@ -1272,7 +1288,7 @@ static int build_dictionary(ii_ctx* c, bool wid = false) {
 // pairs grouped by word, post_start, and the per-word dictionary arrays.
 // wid: sort by word id (single-GPU reduce, k_wid_finish) instead of lexid;
 // the exchange path needs letter-contiguous pairs and sorts by lexid.
-static int local_reduce(ii_ctx* c, bool wid = false) {
+static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     uint64_t* totals = P_<uint64_t>(c->totals);
     (void)totals;
     c->n_sc = 0;
@@ -1344,7 +1360,7 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
         HIPCK(hipMemcpyAsync(c->hbuf, P_<uint64_t>(c->counters) + C_COLLIDE, sizeof(uint64_t), hipMemcpyDeviceToHost,
                              c->st));
     }
-    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_ident ? nullptr : P_<uint32_t>(c->fid)));
+    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_ident ? nullptr : P_<uint32_t>(c->fid), compact));
     if (check) {
         c->lv_pending = false;
         if (c->hbuf[0]) {  // (Las Vegas: the output never depends on the seed)
@@ -1353,7 +1369,7 @@ static int local_reduce(ii_ctx* c, bool wid = false) {
             const uint32_t r0 = c->retries;
             CK(map_core(c, nullptr));
             c->retries += r0 + 1;
-            return local_reduce(c, wid);
+            return local_reduce(c, wid, compact);
         }
     }
     c->wid_pairs = wid;
@@ -1405,12 +1421,21 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     CK(read_u64(c, totals + 2, &c->out_bytes));
     CK(grow(c->out, std::max<uint64_t>(c->out_bytes, 16)));
     uint8_t* out = P_<uint8_t>(c->out);
-    CK(grow(c->fbase, sizeof(uint64_t) * (c->wid_pairs ? c->NW : V)));
+    // fbase by the pairs' word key (wid or lexid), or with compact pairs by the
+    // dense word index (dict_idx of a lexid; lexid keys are dense already)
+    const bool dense_wid = c->pairs32 && c->wid_pairs;
+    CK(grow(c->fbase, sizeof(uint64_t) * (c->wid_pairs && !c->pairs32 ? c->NW : V)));
     uint64_t* fb = P_<uint64_t>(c->fbase);
+    const uint32_t* fkey = dense_wid ? P_<uint32_t>(c->didx) : c->wid_pairs && !c->pairs32 ? P_<uint32_t>(c->widl) : nullptr;
     k_fmt_words<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
-                                                  P_<uint32_t>(c->llen), ps, pe, Pp, loff, (uint32_t)V, out,
-                                                  c->wid_pairs ? P_<uint32_t>(c->widl) : nullptr, fb);
-    k_fmt_posts<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(uniq, c->U, fb, Pp, out);
+                                                  P_<uint32_t>(c->llen), ps, pe, Pp, loff, (uint32_t)V, out, fkey, fb);
+    const uint32_t gfmt = (uint32_t)std::min<uint64_t>(16384, grid_for(c->U));
+    if (c->pairs32)
+        k_fmt_posts<true><<<gfmt, kBlock, 0, c->st>>>(nullptr, P_<uint32_t>(c->uniq), P_<uint32_t>(c->g64),
+                                                      dense_wid ? P_<uint32_t>(c->drank) : nullptr,
+                                                      reinterpret_cast<const uint32_t*>(totals + 7), c->U, fb, Pp, out);
+    else
+        k_fmt_posts<false><<<gfmt, kBlock, 0, c->st>>>(uniq, nullptr, nullptr, nullptr, nullptr, c->U, fb, Pp, out);
     k_letter_off<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), ov, loff, (uint32_t)V, c->out_bytes,
                                       P_<uint64_t>(c->letter_off));
     HIPCK(hipGetLastError());
@@ -1432,15 +1457,16 @@ extern "C" int ii_reduce_local(ii_ctx* c) {
     if (!c) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
-    if (c->have_pairs) return II_OK;
-    return local_reduce(c, true);
+    if (c->have_pairs && !c->pairs32) return II_OK;
+    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;  // an owner's merged pairs are not exported again
+    return local_reduce(c, true, false);
 }
 
 extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     if (!c) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c, true));
+    if (!c->have_pairs) CK(local_reduce(c, true, true));  // formatted only: compact pairs
     return order_and_format(c, copy_text);
 }
 
@@ -1503,7 +1529,8 @@ static int plan_core(ii_ctx* c, int nparts, const int* lo_in, const int* hi_in, 
     }
     if (c->part_hi[nparts - 1] != II_ALPHABET) return II_ERR_ARG;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c, true));
+    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;
+    if (!c->have_pairs || c->pairs32) CK(local_reduce(c, true, false));  // the exchange needs the u64 pairs
     CK(letter_points(c));
     for (int r = 0; r < nparts; r++) {
         const uint64_t* a = c->h_pts + 3 * c->part_lo[r];
@@ -1528,7 +1555,8 @@ extern "C" int ii_letter_load(ii_ctx* c, uint64_t pairs[II_ALPHABET]) {
     if (!c || !pairs) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
     HIPCK(hipSetDevice(c->dev));
-    if (!c->have_pairs) CK(local_reduce(c, true));
+    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;
+    if (!c->have_pairs || c->pairs32) CK(local_reduce(c, true, false));  // the exchange needs the u64 pairs
     CK(letter_points(c));
     for (int l = 0; l < II_ALPHABET; l++) pairs[l] = c->h_pts[3 * (l + 1) + 1] - c->h_pts[3 * l + 1];
     return II_OK;
@@ -1710,7 +1738,7 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
-    CK(run_unique(c, r, NP, false, false, nullptr));  // the owner's merged pairs: dense u64 records of id0s
+    CK(run_unique(c, r, NP, false, false, nullptr, true));  // the owner's merged pairs: dense u64 records of id0s
     HIPCK(hipEventRecord(c->ev[4], c->st));
     c->stats.sort_passes = (uint32_t)(p1 + p2);
     c->have_pairs = true;
@@ -1838,6 +1866,7 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: bytes read + written
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
+        s.pair_bytes = c->pairs32 ? 4u : 8u;
         s.sort_key_bits = (uint32_t)c->sort_W;
         s.sort_id_bits = (uint32_t)c->sort_F;
         s.sorted_records = c->T_sorted;

@@ -1152,12 +1152,19 @@ __global__ void k_check_layout(const uint8_t* __restrict__ text, const uint64_t*
 
 // ---------------------------------------------------------------- dictionary
 // Scan op: compact occupied table slots into dict_slot[].
+// dict_slot[d] = the d-th occupied slot (ascending); rank_hot (optional):
+// rank_hot[s] = d for the occupied hot slots (the compact pairs' formatter
+// turns a group's first word id into its dense index with it)
 struct OpCompactSlots {
     const unsigned long long* keys;
     uint32_t* dict_slot;
+    uint32_t* rank_hot;
     __device__ uint64_t value(uint64_t i) const { return keys[i] != 0ull; }
     __device__ void emit(uint64_t i, uint64_t ex, uint64_t v) const {
-        if (v) dict_slot[ex] = (uint32_t)i;
+        if (v) {
+            dict_slot[ex] = (uint32_t)i;
+            if (rank_hot && i < kHotSlots) rank_hot[i] = (uint32_t)ex;
+        }
     }
 };
 
@@ -1286,18 +1293,26 @@ __global__ __launch_bounds__(kBlock) void k_count_hot(const uint32_t* __restrict
     const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
     if (d < V && dict_slot[d] < kHotSlots && (d + 1 == V || dict_slot[d + 1] >= kHotSlots)) *nhot = d + 1;
 }
-// per lexid j: wid(j); lexw[wid] = j, wmap[slot] = wid for big-table slots
+// wmap[slot] = wid for the big-table slots: kHotSlots + the slot's rank among
+// the occupied big slots (dict_slot ascends; the token sort needs only this)
+__global__ __launch_bounds__(kBlock) void k_wid_map(const uint32_t* __restrict__ dict_slot, uint32_t V,
+                                                    const uint32_t* __restrict__ nhot, uint32_t* __restrict__ wmap) {
+    const uint32_t d = blockIdx.x * kBlock + threadIdx.x;
+    if (d >= V) return;
+    const uint32_t s = dict_slot[d];
+    if (s >= kHotSlots) wmap[s] = (uint32_t)kHotSlots + (d - *nhot);
+}
+// per lexid j: wid(j) (as k_wid_map); lexw[wid] = j, widl[j] = wid
 __global__ __launch_bounds__(kBlock) void k_wid_finish(const uint32_t* __restrict__ dict_idx,
                                                        const uint32_t* __restrict__ dict_slot, uint32_t V,
-                                                       const uint32_t* __restrict__ nhot, uint32_t* __restrict__ wmap,
-                                                       uint32_t* __restrict__ lexw, uint32_t* __restrict__ widl) {
+                                                       const uint32_t* __restrict__ nhot, uint32_t* __restrict__ lexw,
+                                                       uint32_t* __restrict__ widl) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= V) return;
     const uint32_t d = dict_idx[j], s = dict_slot[d];
     const uint32_t wid = s < kHotSlots ? s : (uint32_t)kHotSlots + (d - *nhot);
     lexw[wid] = j;
     widl[j] = wid;
-    if (s >= kHotSlots) wmap[s] = wid;
 }
 
 __global__ __launch_bounds__(kBlock) void k_lex_finish(const uint8_t* __restrict__ text, uint64_t nbytes,
@@ -1599,6 +1614,14 @@ __device__ __forceinline__ void uniq_block_scan(uint32_t c8, uint32_t bl, uint32
     eb = wb + ib - ((uint64_t)bl | (uint64_t)bh << 32);
 }
 
+// Compact pairs (uniq32 != null; the index is formatted, not exported): K3
+// writes each pair as the u32 id0 | kPairFirst when it starts its word, and
+// g64[u / 64] = the word key of pair u at every multiple of 64 — half the
+// bytes of the u64 pairs for K3 to write and the formatter to read.  The
+// words come in key order and every word has a pair, so a pair's word is its
+// group's first word plus the word starts between them (k_fmt_posts<true>).
+constexpr uint32_t kPairFirst = 0x80000000u;
+
 // K3 in one pass (decoupled look-back, as k_onesweep): a workgroup takes a
 // tile of kUniqSub sub-tiles (kUniqTile records each) from a ticket, scans
 // them, publishes the tile's distinct
@@ -1628,7 +1651,8 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                                                        uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
                                                        uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err,
-                                                       const uint32_t* __restrict__ fmap) {
+                                                       const uint32_t* __restrict__ fmap, uint32_t* __restrict__ uniq32,
+                                                       uint32_t* __restrict__ g64) {
     // the tile staged in LDS (scanned, then written after the look-back): u64
     // records from [1] with the record before the tile at [0], or in the packed
     // form the raw u32 records (16 KiB, 8 workgroups per CU instead of 3) and
@@ -1833,8 +1857,13 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                 item(k, q, r, pv);
                 const uint64_t uu = rc + (f & 0x7FFFull);
                 const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
-                uniq[uu] = (r & ~0xFFFFFFFFull) | file_id0(fmap, (uint32_t)r);
                 const bool wstart = pv == ~0ull || key != pkey;
+                if (uniq32) {  // (uniform)
+                    uniq32[uu] = file_id0(fmap, (uint32_t)r) | (wstart ? kPairFirst : 0u);
+                    if ((uu & 63u) == 0) g64[uu >> 6] = key;
+                } else {
+                    uniq[uu] = (r & ~0xFFFFFFFFull) | file_id0(fmap, (uint32_t)r);
+                }
                 // P is read at word starts (k_fmt_words, OpLineOff) and at the
                 // first posting of every 64 (k_fmt_posts) only
                 if (wstart || (uu & 63u) == 0) P[uu] = rb + ((eb >> (16 * q)) & 0xFFFFull);
@@ -1945,48 +1974,84 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
 // places the rest by a wave scan of their byte counts, so the pass reads
 // 8 bytes per posting instead of 16.
 constexpr int kFmtItems = 4;  // groups per wave (2 or 8: slower)
-__global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restrict__ uniq, uint64_t U,
+// k32: the compact pairs (uniq32 / g64, k_uniq_sweep): a group's first word
+// key -> its dense index d (rank_hot for a hot word id, nhot + (key -
+// kHotSlots) for a big-table one, the key itself for lexid keys: rank_hot
+// null), the word of lane i = d + the word starts in lanes 1..i, and fbase is
+// indexed by d.
+template <bool k32>
+__global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restrict__ uniq,
+                                                      const uint32_t* __restrict__ uniq32,
+                                                      const uint32_t* __restrict__ g64,
+                                                      const uint32_t* __restrict__ rank_hot,
+                                                      const uint32_t* __restrict__ nhot, uint64_t U,
                                                       const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
                                                       uint8_t* __restrict__ out) {
     constexpr uint64_t kSpan = 64ull * kFmtItems;  // postings of one wave per iteration
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const int l = lane_id();
+    const uint64_t le = ~0ull >> (63 - l);  // lanes 0..l
+    const uint32_t nh = k32 && rank_hot ? *nhot : 0u;
     for (uint64_t g0 = ((uint64_t)blockIdx.x * kWaves + (uint64_t)wave_id()) * kSpan; g0 < U; g0 += nwaves * kSpan) {
         uint64_t r[kFmtItems], pb[kFmtItems], fb[kFmtItems];
-        uint32_t wn[kFmtItems];
+        uint32_t wn[kFmtItems];  // k32: 1 if the posting after this one starts a word; else its word
+        uint32_t x[kFmtItems], wd[kFmtItems];
 #pragma unroll
         for (int k = 0; k < kFmtItems; k++) {
-            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
-            r[k] = p < U ? uniq[p] : 0ull;
+            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)l;
+            if (k32) {
+                x[k] = p < U ? uniq32[p] : kPairFirst;
+                wd[k] = g0 + (uint64_t)k * 64 < U ? g64[(g0 >> 6) + k] : 0u;
+            } else {
+                r[k] = p < U ? uniq[p] : 0ull;
+            }
             pb[k] = g0 + (uint64_t)k * 64 < U ? P[g0 + (uint64_t)k * 64] : 0ull;
         }
-        // word of the posting after each group's lane 63 (the next group's lane 0)
+        // the posting after each group's lane 63 (the next group's lane 0)
         const uint64_t pn = g0 + kSpan;
-        const uint32_t wtail = (lane_id() == 63 && pn < U) ? (uint32_t)(uniq[pn] >> 32) : 0u;
+        uint32_t xtail = kPairFirst, wtail = 0u;
+        if (l == 63 && pn < U) {
+            if (k32) xtail = uniq32[pn];
+            else wtail = (uint32_t)(uniq[pn] >> 32);
+        }
+        if (k32) {
 #pragma unroll
-        for (int k = 0; k < kFmtItems; k++) {
-            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
-            fb[k] = p < U ? fbase[(uint32_t)(r[k] >> 32)] : 0ull;
+            for (int k = 0; k < kFmtItems; k++) {
+                const uint32_t w0 = wd[k];
+                const uint32_t d0 = !rank_hot ? w0 : w0 < (uint32_t)kHotSlots ? rank_hot[w0] : nh + (w0 - (uint32_t)kHotSlots);
+                const uint64_t fm = __ballot((x[k] & kPairFirst) != 0u);
+                const uint32_t d = d0 + (uint32_t)__popcll(fm & le & ~1ull);
+                const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)l;
+                fb[k] = p < U ? fbase[d] : 0ull;
+                const uint32_t nx = k + 1 < kFmtItems ? (uint32_t)__shfl((int)x[k + 1 < kFmtItems ? k + 1 : k], 0, 64) : xtail;
+                wn[k] = l == 63 ? (nx >> 31) : (uint32_t)(fm >> (l + 1)) & 1u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kFmtItems; k++) {
+                const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)l;
+                fb[k] = p < U ? fbase[(uint32_t)(r[k] >> 32)] : 0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < kFmtItems; k++) {
+                const uint32_t w = (uint32_t)(r[k] >> 32);
+                uint32_t d = __shfl_down(w, 1, 64);
+                const uint32_t first_next = k + 1 < kFmtItems ? __shfl((uint32_t)(r[k + 1 < kFmtItems ? k + 1 : k] >> 32), 0, 64)
+                                                              : wtail;
+                wn[k] = l == 63 ? first_next : d;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kFmtItems; k++) {
-            const uint32_t w = (uint32_t)(r[k] >> 32);
-            uint32_t d = __shfl_down(w, 1, 64);
-            const uint32_t first_next = k + 1 < kFmtItems ? __shfl((uint32_t)(r[k + 1 < kFmtItems ? k + 1 : k] >> 32), 0, 64)
-                                                          : wtail;
-            wn[k] = lane_id() == 63 ? first_next : d;
-        }
-#pragma unroll
-        for (int k = 0; k < kFmtItems; k++) {
-            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)lane_id();
+            const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)l;
             const bool live = p < U;
-            const uint32_t w = (uint32_t)(r[k] >> 32);
-            const uint64_t id = (r[k] & 0xFFFFFFFFull) + 1;
+            const uint64_t id = k32 ? (uint64_t)(x[k] & ~kPairFirst) + 1 : (r[k] & 0xFFFFFFFFull) + 1;
             const uint32_t nd = id_digits(id);
             const uint32_t len = live ? nd + 1u : 0u;
             const uint32_t inc = wave_incl_scan32(len);  // inclusive wave scan (64 postings x <= 11 bytes)
             if (!live) continue;
             // last posting of the word: the next pair belongs to another word (runs are contiguous)
-            const bool last = p + 1 == U || wn[k] != w;
+            const bool last = p + 1 == U || (k32 ? wn[k] != 0u : wn[k] != (uint32_t)(r[k] >> 32));
             const uint64_t o = fb[k] + pb[k] + (inc - len);
             if (nd <= 7u) {
                 // digits + separator (<= 8 bytes) built in one register (each lower digit pushes

@@ -89,12 +89,24 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total,
 //   void     emit(uint64_t i, uint64_t excl, uint64_t value)
 // Items are handled per chunk; per-chunk sums land in `partial`.
 // ----------------------------------------------------------------------------
+// Both passes keep several items per thread in flight: the reduce sums four
+// strided items per iteration (independent loads), the apply gives every
+// thread kScanItems consecutive items — a serial prefix in registers and one
+// block scan per 2048 items instead of one per 256 (the per-256 form ran the
+// dictionary's 5.2 M-slot compaction scan at 0.5 ms, latency-bound).
+constexpr int kScanItems = 8;
 template <class Op>
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(Op op, uint64_t n, uint64_t chunk, uint64_t* partial) {
     __shared__ uint64_t lds[kWaves + 1];
     uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint64_t acc = 0;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) acc += op.value(i);
+    uint64_t i = lo + threadIdx.x;
+    for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
+        const uint64_t a = op.value(i), b = op.value(i + kBlock), c = op.value(i + 2 * kBlock),
+                       d = op.value(i + 3 * kBlock);
+        acc += (a + b) + (c + d);
+    }
+    for (; i < hi; i += kBlock) acc += op.value(i);
     acc = wave_sum(acc);
     if (lane_id() == 0) lds[wave_id()] = acc;
     __syncthreads();
@@ -133,12 +145,22 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(Op op, uint64_t n, uint64
     __shared__ uint64_t lds[kWaves + 1];
     uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint64_t run = partial[blockIdx.x];
-    for (uint64_t base = lo; base < hi; base += kBlock) {
-        uint64_t i = base + threadIdx.x;
-        uint64_t v = i < hi ? op.value(i) : 0;
+    for (uint64_t base = lo; base < hi; base += (uint64_t)kBlock * kScanItems) {
+        const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanItems;
+        uint64_t v[kScanItems];
+        uint64_t s = 0;
+#pragma unroll
+        for (int j = 0; j < kScanItems; j++) {
+            v[j] = i0 + j < hi ? op.value(i0 + j) : 0;
+            s += v[j];
+        }
         uint64_t tot;
-        uint64_t ex = block_excl_scan(v, &tot, lds);
-        if (i < hi) op.emit(i, run + ex, v);
+        uint64_t ex = run + block_excl_scan(s, &tot, lds);
+#pragma unroll
+        for (int j = 0; j < kScanItems; j++) {
+            if (i0 + j < hi) op.emit(i0 + j, ex, v[j]);
+            ex += v[j];
+        }
         run += tot;
     }
 }
