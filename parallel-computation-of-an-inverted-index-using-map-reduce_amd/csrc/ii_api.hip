@@ -806,12 +806,11 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
-        k_tok_emit<<<wg_chunks, kBlock, 0, c->st>>>(c->text, c->nbytes, nch, fstart, chunk_cnt,
-                                                       c->rec_cap, tab,
-                                                       P_<uint64_t>(c->rec), P_<uint32_t>(c->chunk_hist),
-                                                       P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt),
-                                                       P_<uint32_t>(c->chunk_files), P_<LongTok>(c->longs),
-                                                       c->long_cap / kLongShards, narrow_keys());
+        const uint32_t nkeys = narrow_keys();
+        (nkeys == kNarrowKeys ? k_tok_emit<false> : k_tok_emit<true>)<<<wg_chunks, kBlock, 0, c->st>>>(
+            c->text, c->nbytes, nch, fstart, chunk_cnt, c->rec_cap, tab, P_<uint64_t>(c->rec),
+            P_<uint32_t>(c->chunk_hist), P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), P_<uint32_t>(c->chunk_files),
+            P_<LongTok>(c->longs), c->long_cap / kLongShards, nkeys);
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         k_long_totals<<<1, 64, 0, c->st>>>(counters);
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));
@@ -1306,9 +1305,12 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     // its lexicographic part (a sort of the V prefix keys, ~0.5 ms of small
     // launches and host round trips) runs on st2 beside the sort, queued once
     // the sort is; K3's word-id -> lexid step waits for it
-    if (wid) {
+    const bool dict_side = wid;  // (same-box A/B: 394.0-394.5 GB/s with the dictionary in stream order, 395.6-396.3 beside the sort)
+    if (dict_side) {
         CK(dict_slots(c, true));
         HIPCK(hipEventRecord(c->ev_dict[0], c->st));
+    } else if (wid) {
+        CK(build_dictionary(c, true));
     } else {
         CK(build_dictionary(c, false));
     }
@@ -1334,7 +1336,7 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     c->rec_sorted = r;
     c->T_sorted = Tk;
     HIPCK(hipEventRecord(c->ev[3], c->st));
-    if (wid) {
+    if (dict_side) {
         HIPCK(hipEventSynchronize(c->ev_dict[0]));  // (the sort's own synchronisation is past it already)
         if (c->hbuf[1] != V) return II_ERR_INTERNAL;
         {
@@ -1430,12 +1432,16 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     k_fmt_words<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
                                                   P_<uint32_t>(c->llen), ps, pe, Pp, loff, (uint32_t)V, out, fkey, fb);
     const uint32_t gfmt = (uint32_t)std::min<uint64_t>(16384, grid_for(c->U));
-    if (c->pairs32)
-        k_fmt_posts<true><<<gfmt, kBlock, 0, c->st>>>(nullptr, P_<uint32_t>(c->uniq), P_<uint32_t>(c->g64),
-                                                      dense_wid ? P_<uint32_t>(c->drank) : nullptr,
-                                                      reinterpret_cast<const uint32_t*>(totals + 7), c->U, fb, Pp, out);
-    else
-        k_fmt_posts<false><<<gfmt, kBlock, 0, c->st>>>(uniq, nullptr, nullptr, nullptr, nullptr, c->U, fb, Pp, out);
+    if (c->pairs32) {
+        const uint64_t ng = (c->U + 63) / 64;
+        if (dense_wid)
+            k_g64_dense<<<grid_for(ng), kBlock, 0, c->st>>>(P_<uint32_t>(c->g64), ng, P_<uint32_t>(c->drank),
+                                                           reinterpret_cast<const uint32_t*>(totals + 7));
+        k_fmt_posts<true><<<gfmt, kBlock, 0, c->st>>>(nullptr, P_<uint32_t>(c->uniq), P_<uint32_t>(c->g64), c->U, fb,
+                                                      Pp, out);
+    } else {
+        k_fmt_posts<false><<<gfmt, kBlock, 0, c->st>>>(uniq, nullptr, nullptr, c->U, fb, Pp, out);
+    }
     k_letter_off<<<1, 64, 0, c->st>>>(P_<uint32_t>(c->lstart), ov, loff, (uint32_t)V, c->out_bytes,
                                       P_<uint64_t>(c->letter_off));
     HIPCK(hipGetLastError());

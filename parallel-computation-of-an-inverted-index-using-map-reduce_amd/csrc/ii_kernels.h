@@ -856,10 +856,7 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
                                                uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
                                                const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
-                                               uint64_t long_per, uint32_t narrow_keys, EmitLds* s_lds) {
-    const uint64_t c = wave_chunk();
-    if (c >= nch) return;
-    EmitLds& W = s_lds[c - (uint64_t)blockIdx.x * kWG];
+                                               uint64_t long_per, uint32_t narrow_keys, uint64_t c, EmitLds& W) {
     const int l = lane_id();
     const uint64_t chunk_lo = c * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
@@ -873,6 +870,7 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
     uint32_t out = 0;               // records emitted so far (wave-uniform)
     uint32_t npf = 0, nps = 0;      // tokens left to K1c: fast-path misses, general-path tokens
     const uint64_t pend_end = pend_limit(chunk_off, cap, cbase, c);
+    const uint32_t nk_lim = narrow ? narrow_keys : ~0u;  // (a bound held in a register, not a kernel argument re-read per batch)
     if (l < 32) W.hist[l] = 0;
     RoundRegs nxt;
     fetch_round(nxt, text, nbytes, chunk_lo);
@@ -941,7 +939,7 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
             const bool resolved = fast && slot != kSlotNone;
             bool pf = fast && !resolved, ps = valid && !fast;
             uint64_t mf = __ballot(pf);
-            if (narrow && npf + (uint32_t)__popcll(mf) > narrow_keys) {  // (wave-uniform, adversarial) no room for
+            if (npf + (uint32_t)__popcll(mf) > nk_lim) {  // (wave-uniform, adversarial) no room for
                 if (pf) atomicSub(&W.hist[tk.first], 1u);                     // more keys: K1c re-reads them from the
                 ps = ps || pf;                                                // text (and counts their letters)
                 pf = false;
@@ -988,6 +986,10 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
 // K1b.  Launch bound of 8 waves per SIMD: it caps the SGPRs at 78 (52 spilled
 // to VGPR lanes); at the compiler's own 106 SGPRs the SGPR file held 7 waves
 // per SIMD and the pass ran 12.35 ms instead of 11.70 at 10 GB.
+// kKeysArg: the narrow chunks' key capacity comes from the argument (the
+// II_NARROW_KEYS test knob); otherwise it is the constant kNarrowKeys (the
+// SGPR-capped kernel re-read the argument from memory once per batch).
+template <bool kKeysArg>
 __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                      const uint64_t* __restrict__ file_start,
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
@@ -996,8 +998,13 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
                                                      const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
                                                      uint64_t long_per, uint32_t narrow_keys) {
     __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
-    tok_emit_chunk<HotProbe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
-                             longs, long_per, narrow_keys, s_lds);
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // one chunk per wave (waves that loop over chunks, a grid of the resident workgroups: emit 11.46 -> 12.98 ms
+    // at 10 GB, same-box A/B)
+    const uint64_t c = (uint64_t)blockIdx.x * kWG + w;
+    if (c < nch)
+        tok_emit_chunk<HotProbe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
+                                 longs, long_per, kKeysArg ? narrow_keys : kNarrowKeys, c, s_lds[w]);
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
@@ -1067,24 +1074,35 @@ struct LetterCursor {
 // byte mask (0xFF per selected byte) of the low 4 bits of m, one bit per byte
 __device__ __forceinline__ uint32_t byte_mask4(uint32_t m) { return ((m & 0xFu) * 0x00204081u & 0x01010101u) * 0xFFu; }
 
-// Two tokens whose raw bytes agree up to their first whitespace / NUL, letters
-// compared case-insensitively, clean to the same word (main.c:105-111).
-// Returns 1 = same word, 0 = undecided (the letter walk decides).
+// Two tokens whose raw bytes agree up to their last letter (letters compared
+// case-insensitively; what follows the last letter is dropped by the cleaning
+// loop, main.c:105-111, so trailing punctuation may differ) clean to the same
+// word.  Returns 1 = same word, 0 = undecided (the letter walk decides): a
+// token that ends in a block where the other does not, or bytes that differ
+// before the last letter.  (Comparing up to the first whitespace sent every
+// occurrence with a trailing '.', ',' ... — 5 % of the corpus's tokens — to
+// the letter walk, which held whole waves.)
 __device__ __forceinline__ int same_raw_token(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t a, uint64_t b) {
     for (uint32_t off = 0; off < 4 * (uint32_t)kMaxWord; off += 16) {
         const uint4 A = global_block16(text, nbytes, a + off), B = global_block16(text, nbytes, b + off);
         const Classes ca = classify16(A), cb = classify16(B);
         const uint32_t ta = ca.ws | ca.nul, tb = cb.ws | cb.nul;
         const uint32_t ea = ta ? __builtin_ctz(ta) : 16u, eb = tb ? __builtin_ctz(tb) : 16u;
-        if (ea != eb) return 0;
-        const uint32_t live = ea == 16u ? 0xFFFFu : (1u << ea) - 1u;
-        if ((ca.letter ^ cb.letter) & live) return 0;
+        if ((ea == 16u) != (eb == 16u)) return 0;
+        uint32_t m = 0xFFFFu;  // bytes that must agree
+        const uint32_t la = ca.letter & ((1u << ea) - 1u), lb = cb.letter & ((1u << eb) - 1u);
+        if (ea < 16u) {  // both end here: compare up to the last letter (none: the earlier blocks decided)
+            const int za = la ? 31 - __builtin_clz(la) : -1, zb = lb ? 31 - __builtin_clz(lb) : -1;
+            if (za != zb) return 0;
+            m = za < 0 ? 0u : (2u << za) - 1u;
+        }
+        if ((la ^ lb) & m) return 0;
         const uint32_t wa[4] = {A.x, A.y, A.z, A.w}, wb[4] = {B.x, B.y, B.z, B.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t lowa = wa[k] | (byte_mask4(ca.letter >> (4 * k)) & 0x20202020u);
             const uint32_t lowb = wb[k] | (byte_mask4(cb.letter >> (4 * k)) & 0x20202020u);
-            if ((lowa ^ lowb) & byte_mask4(live >> (4 * k))) return 0;
+            if ((lowa ^ lowb) & byte_mask4(m >> (4 * k))) return 0;
         }
         if (ea < 16u) return 1;
     }
@@ -1973,25 +1991,34 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
 // only (P is written at multiples of 64 and at word starts, k_uniq_sweep) and
 // places the rest by a wave scan of their byte counts, so the pass reads
 // 8 bytes per posting instead of 16.
+// g64[g] (a word id, compact pairs of a word-id sort) -> the word's dense
+// index (its rank among the occupied slots): one pass over U / 64 entries, so
+// that the formatter's chain stays group key -> fbase (a rank gather in it
+// made the pass 1.64 -> 1.9 ms, one more dependent load per group)
+__global__ __launch_bounds__(kBlock) void k_g64_dense(uint32_t* __restrict__ g64, uint64_t n,
+                                                      const uint32_t* __restrict__ rank_hot,
+                                                      const uint32_t* __restrict__ nhot) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= n) return;
+    const uint32_t w = g64[g];
+    g64[g] = w < (uint32_t)kHotSlots ? rank_hot[w] : *nhot + (w - (uint32_t)kHotSlots);
+}
+
 constexpr int kFmtItems = 4;  // groups per wave (2 or 8: slower)
-// k32: the compact pairs (uniq32 / g64, k_uniq_sweep): a group's first word
-// key -> its dense index d (rank_hot for a hot word id, nhot + (key -
-// kHotSlots) for a big-table one, the key itself for lexid keys: rank_hot
-// null), the word of lane i = d + the word starts in lanes 1..i, and fbase is
-// indexed by d.
+// k32: the compact pairs (uniq32 / g64, k_uniq_sweep): g64 holds each
+// group's first word as a dense index d (k_g64_dense; lexid keys are dense
+// already), the word of lane i = d + the word starts in lanes 1..i, and fbase
+// is indexed by d.
 template <bool k32>
 __global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restrict__ uniq,
                                                       const uint32_t* __restrict__ uniq32,
-                                                      const uint32_t* __restrict__ g64,
-                                                      const uint32_t* __restrict__ rank_hot,
-                                                      const uint32_t* __restrict__ nhot, uint64_t U,
+                                                      const uint32_t* __restrict__ g64, uint64_t U,
                                                       const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ P,
                                                       uint8_t* __restrict__ out) {
     constexpr uint64_t kSpan = 64ull * kFmtItems;  // postings of one wave per iteration
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     const int l = lane_id();
     const uint64_t le = ~0ull >> (63 - l);  // lanes 0..l
-    const uint32_t nh = k32 && rank_hot ? *nhot : 0u;
     for (uint64_t g0 = ((uint64_t)blockIdx.x * kWaves + (uint64_t)wave_id()) * kSpan; g0 < U; g0 += nwaves * kSpan) {
         uint64_t r[kFmtItems], pb[kFmtItems], fb[kFmtItems];
         uint32_t wn[kFmtItems];  // k32: 1 if the posting after this one starts a word; else its word
@@ -2017,8 +2044,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restr
         if (k32) {
 #pragma unroll
             for (int k = 0; k < kFmtItems; k++) {
-                const uint32_t w0 = wd[k];
-                const uint32_t d0 = !rank_hot ? w0 : w0 < (uint32_t)kHotSlots ? rank_hot[w0] : nh + (w0 - (uint32_t)kHotSlots);
+                const uint32_t d0 = wd[k];
                 const uint64_t fm = __ballot((x[k] & kPairFirst) != 0u);
                 const uint32_t d = d0 + (uint32_t)__popcll(fm & le & ~1ull);
                 const uint64_t p = g0 + (uint64_t)k * 64 + (uint64_t)l;

@@ -104,8 +104,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __res
                                                          const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
                                                          uint64_t long_per, uint32_t narrow_keys) {
     __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
-    tok_emit_chunk<Probe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf, longs,
-                          long_per, narrow_keys, s_lds);
+    const uint64_t c = wave_chunk();
+    if (c < nch)
+        tok_emit_chunk<Probe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
+                              longs, long_per, narrow_keys, c, s_lds[c - (uint64_t)blockIdx.x * kWG]);
 }
 
 template <class Probe>
