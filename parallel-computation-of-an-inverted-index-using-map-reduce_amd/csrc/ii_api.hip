@@ -39,6 +39,7 @@ struct ii_ctx {
     bool lv_pending = false;    // a k_long_verify on st2 whose verdict the host has not read yet (ev_res[1])
     bool test_collide = false;  // test knob II_TEST_COLLIDE=1: the first check of the context reports a collision
     uint32_t collide_retries = 0;
+    int test_long_bits = 64;    // test knob II_TEST_LONG_KEY_BITS=b: the first map of a context hashes long words to b bits
     uint64_t* hbuf = nullptr;   // pinned host words for readbacks queued before a later sync
 
     // input
@@ -634,6 +635,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     }
     c->test_lb_timeout = getenv("II_TEST_LB_TIMEOUT") && !strcmp(getenv("II_TEST_LB_TIMEOUT"), "1");
     c->test_collide = getenv("II_TEST_COLLIDE") && !strcmp(getenv("II_TEST_COLLIDE"), "1");
+    if (getenv("II_TEST_LONG_KEY_BITS")) c->test_long_bits = std::min(64, std::max(0, atoi(getenv("II_TEST_LONG_KEY_BITS"))));
     const char* s = getenv("II_TABLE_LOG2");
     if (s && atoi(s) >= 10 && atoi(s) <= 30) c->big_cap = 1ull << atoi(s);
     memset(&c->stats, 0, sizeof(c->stats));
@@ -804,7 +806,9 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(grow(c->longs, sizeof(LongTok) * c->long_cap));
         HIPCK(hipMemsetAsync(c->tkeys.p, 0, sizeof(uint64_t) * nslots, c->st));
         HIPCK(hipMemsetAsync(counters, 0, sizeof(uint64_t) * C_NUM, c->st));
-        Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters};
+        // (the test knob: real collisions between different long words, until the first retry)
+        const uint64_t long_mask = c->test_long_bits < 64 && c->collide_retries == 0 ? (1ull << c->test_long_bits) - 1ull : ~0ull;
+        Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters, long_mask};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
         const uint32_t nkeys = narrow_keys();
         (nkeys == kNarrowKeys ? k_tok_emit<false> : k_tok_emit<true>)<<<wg_chunks, kBlock, 0, c->st>>>(
@@ -840,6 +844,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
             continue;
         }
         if (cnt[C_COLLIDE]) {  // two long words hashed alike: new seed, redo (Las Vegas)
+            if (++c->collide_retries > 12) return II_ERR_INTERNAL;
             c->seed = c->seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull;
             c->retries++;
             continue;

@@ -85,6 +85,7 @@ struct Table {
     uint64_t big_mask;         // big_cap - 1
     uint64_t seed;
     uint64_t* counters;
+    uint64_t long_mask;        // hashed keys keep these bits of the hash (~0; fewer: the II_TEST_LONG_KEY_BITS test knob)
 };
 
 // Home slot of a key in the hot table: a 32-bit multiply-xorshift hash of the
@@ -174,8 +175,8 @@ __device__ __forceinline__ LongWord read_word(const uint8_t* __restrict__ text, 
     return w;
 }
 
-__device__ __forceinline__ uint64_t long_key(uint64_t hash, uint32_t len, uint64_t seed) {
-    return (mix64(hash ^ seed ^ ((uint64_t)len << 48)) << 4) | 0xFull;
+__device__ __forceinline__ uint64_t long_key(uint64_t hash, uint32_t len, uint64_t seed, uint64_t mask) {
+    return ((mix64(hash ^ seed ^ ((uint64_t)len << 48)) & mask) << 4) | 0xFull;
 }
 
 // Reader of the staged tile: tile-local byte j (j >= -16); LDS is read one
@@ -696,7 +697,7 @@ struct LetterStream {
     }
 };
 __device__ __forceinline__ TokKey general_key(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t pos,
-                                              uint64_t seed) {
+                                              uint64_t seed, uint64_t long_mask) {
     LetterStream st{1469598103934665603ull ^ seed, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     uint64_t g = pos & ~15ull;
     uint32_t below = (1u << (pos & 15u)) - 1u;  // first block: bytes before the token
@@ -751,7 +752,7 @@ __device__ __forceinline__ TokKey general_key(const uint8_t* __restrict__ text, 
     if (st.pc) st.fold(st.pend);
     const uint64_t key = st.n <= 12 ? ((uint64_t)pack4(st.d0) << 44) | ((uint64_t)pack4(st.d1) << 24) |
                                           ((uint64_t)pack4(st.d2) << 4)
-                                    : long_key(st.hash, st.n, seed);
+                                    : long_key(st.hash, st.n, seed, long_mask);
     return TokKey{key, st.n, st.n ? (st.d0 & 31u) - 1u : 0u};
 }
 
@@ -782,7 +783,7 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
             const uint32_t jr = ((e >> 16) + rot) & wrap;  // the token's record in the chunk's slot
             uint64_t key;
             if (kSlow) {
-                const TokKey k = general_key(text, nbytes, pos, tab.seed);
+                const TokKey k = general_key(text, nbytes, pos, tab.seed, tab.long_mask);
                 atomicAdd(&hist[k.first], 1u);
                 key = k.key;
                 is_long = k.nlet > 12;

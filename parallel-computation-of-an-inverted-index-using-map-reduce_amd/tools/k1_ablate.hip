@@ -169,7 +169,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&rec, 8 * T));
     uint32_t *pend, *pcnt;
     CK(hipMalloc(&pend, 4 * T)); CK(hipMalloc(&pcnt, 4 * nch));
-    Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters};
+    Table tab{keys, rep, big - 1, 0x51ed270b27a3f3c1ull, counters, ~0ull};
 #define RUNW(A, name, warm) do { float e_ = run<A>(d_text, nb, fstart, fid, p.nfiles, chunk, tab, nslots, rec, chist, longs, lcap, nch, pend, pcnt, warm); \
     unsigned long long np_ = 0; std::vector<uint32_t> pc_(nch); CK(hipMemcpy(pc_.data(), pcnt, 4 * nch, hipMemcpyDeviceToHost)); \
     for (auto x : pc_) np_ += (x & 0xFFFFu) + (x >> 16); \

@@ -497,3 +497,52 @@ def test_long_word_collision_retry():
             assert ix.stats().retries >= 1
     finally:
         os.environ.pop("II_TEST_COLLIDE", None)
+
+
+# ---------------------------------------------------------------- exactness of hashed (> 12-letter) keys
+# II_TEST_LONG_KEY_BITS=0 makes the first map of a context hash every long
+# word to ONE key, so two different long words really collide: the check
+# (k_long_verify: raw bytes up to the last letter, else the letter walk) must
+# flag it — a retry with full keys — and must not flag raw forms of one word
+# (case, trailing punctuation, inner apostrophes, a leading bracket).
+ONE_WORD = [b"internationalization", b"Internationalization.", b"INTERNATIONALIZATION,", b"(internationalization",
+            b"inter'nationalization", b"internationalization!?", b"InTeRnAtIoNaLiZaTiOn;"]
+COLLIDE_CASES = {
+    "one_word": (ONE_WORD, False),
+    "two_words": (ONE_WORD + [b"characterizations"], True),
+    "plural": (ONE_WORD + [b"internationalizations."], True),   # one more letter after the shared ones
+    "after_punct": (ONE_WORD + [b"internationalization.x"], True),  # a letter after trailing punctuation
+}
+
+
+def collide_corpus(forms, nfiles=24, seed=7):
+    rng = random.Random(seed)
+    short = [b"the", b"of", b"and", b"Word", b"a", b"zebra", b"it's"]
+    text = bytearray()
+    off = [0]
+    for f in range(nfiles):
+        toks = [rng.choice(forms) if rng.random() < 0.3 else rng.choice(short) for _ in range(400 + 37 * f)]
+        toks[f % len(toks)] = forms[f % len(forms)]  # every form occurs
+        text += b" ".join(toks) + b"\n"
+        off.append(len(text))
+    return bytes(text), off, list(range(nfiles))
+
+
+@pytest.mark.parametrize("case", sorted(COLLIDE_CASES))
+def test_long_key_collisions_detected(case):
+    forms, collide = COLLIDE_CASES[case]
+    text, off, ids = collide_corpus(forms)
+    exp = oracle_index(text, off, ids)
+    os.environ["II_TEST_LONG_KEY_BITS"] = "0"
+    try:
+        with ii_ctypes.Index(0) as ix:
+            ix.map_host(text, off, ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, "long-key collisions %s" % case)
+            retries = ix.stats().retries
+        assert (retries >= 1) == collide, "%s: %d map retries" % (case, retries)
+        # the same through G = 3 logical shards: the owners' import maps the received words densely
+        got = shard_and_merge(text, off, 3)
+        assert_same(got, exp, "long-key collisions %s, 3 shards" % case)
+    finally:
+        os.environ.pop("II_TEST_LONG_KEY_BITS", None)
