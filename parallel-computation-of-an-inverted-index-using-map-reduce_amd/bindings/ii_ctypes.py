@@ -42,7 +42,7 @@ class Stats(ctypes.Structure):
         ("io_ms", ctypes.c_double), ("io_bytes", ctypes.c_uint64),
         ("sort_bytes", ctypes.c_uint64), ("sort_packed", ctypes.c_uint32),
         ("sort_key_bits", ctypes.c_uint32), ("sort_id_bits", ctypes.c_uint32),
-        ("pair_bytes", ctypes.c_uint32),
+        ("pair_bytes", ctypes.c_uint32), ("deep_probe", ctypes.c_uint32),
     ]
 
     def as_dict(self):

@@ -122,6 +122,8 @@ struct ii_ctx {
     uint32_t pk_nb = 0, pk_ntb = 0;
     int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
+    bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
+    bool map_deep = false;   // the last map ran K1b with DeepProbe
     uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
     uint64_t nch_map = 0;   // K1b chunks of the last map
     // pipelined file reader (ii_map_files): per thread a stream and two pinned windows
@@ -811,7 +813,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         Table tab{P_<unsigned long long>(c->tkeys), P_<uint64_t>(c->trep), c->big_cap - 1, c->seed, counters, long_mask};
         HIPCK(hipEventRecord(c->ev_emit[0], c->st));
         const uint32_t nkeys = narrow_keys();
-        (nkeys == kNarrowKeys ? k_tok_emit<false> : k_tok_emit<true>)<<<wg_chunks, kBlock, 0, c->st>>>(
+        c->map_deep = c->deep_probe;
+        auto* emit = nkeys == kNarrowKeys ? (c->deep_probe ? k_tok_emit<false, true> : k_tok_emit<false, false>)
+                                          : (c->deep_probe ? k_tok_emit<true, true> : k_tok_emit<true, false>);
+        emit<<<wg_chunks, kBlock, 0, c->st>>>(
             c->text, c->nbytes, nch, fstart, chunk_cnt, c->rec_cap, tab, P_<uint64_t>(c->rec),
             P_<uint32_t>(c->chunk_hist), P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), P_<uint32_t>(c->chunk_files),
             P_<LongTok>(c->longs), c->long_cap / kLongShards, nkeys);
@@ -1340,6 +1345,9 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
                     P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid));
     c->rec_sorted = r;
     c->T_sorted = Tk;
+    // the next map's probe depth: DeepProbe when most distinct words live in the big table (NW = the
+    // hot slots + the big-table words; wid keys only: lexid keys leave the choice as it was)
+    if (wid) c->deep_probe = 2 * (c->NW - kHotSlots) > V;
     HIPCK(hipEventRecord(c->ev[3], c->st));
     if (dict_side) {
         HIPCK(hipEventSynchronize(c->ev_dict[0]));  // (the sort's own synchronisation is past it already)
@@ -1878,6 +1886,7 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
         s.pair_bytes = c->pairs32 ? 4u : 8u;
+        s.deep_probe = c->map_deep ? 1u : 0u;
         s.sort_key_bits = (uint32_t)c->sort_W;
         s.sort_id_bits = (uint32_t)c->sort_F;
         s.sorted_records = c->T_sorted;

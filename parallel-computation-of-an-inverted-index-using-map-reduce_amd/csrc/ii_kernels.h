@@ -849,7 +849,49 @@ struct HotProbe {
     }
 };
 
-// K1b for the chunk of this wave (the kernel body; Probe: HotProbe in the product).
+// The probe for vocabularies larger than the hot level (DeepProbe, chosen by
+// the host when most of the previous map's distinct words lived in the big
+// table — configs[4]'s vocabulary of 10^7 against 2^20 hot slots): a lane
+// whose two pairs are full without its key loads the bucket's other two pairs
+// and its big-table home slot in one more round trip, so a word resolved at
+// its big home (found, or claimed there: table_find's rule, whose linear
+// probe starts at the home) no longer goes to the K1c tail; only words past
+// their big home do.  (With a vocabulary that fits the hot level the extra
+// round trip costs more than the few K1c tokens it saves: emit +0.2 ms at 10 GB.)
+struct DeepProbe {
+    __device__ __forceinline__ ProbeState begin(const Table& t, bool fast, uint64_t key, uint32_t home) const {
+        return HotProbe().begin(t, fast, key, home);
+    }
+    __device__ __forceinline__ uint32_t finish(const Table& t, const ProbeState& st, bool fast, uint64_t key,
+                                              uint64_t pos) const {
+        const uint32_t bbase = st.home & ~(uint32_t)(kBucket - 1), start = st.home & (kBucket - 2);
+        uint32_t match = (uint32_t)(st.qa.x == key) | ((uint32_t)(st.qa.y == key) << 1);
+        uint32_t empty = (uint32_t)(st.qa.x == 0ull) | ((uint32_t)(st.qa.y == 0ull) << 1);
+        if (fast && !(match | empty)) {
+            const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
+            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
+            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
+        }
+        if (fast && !(match | empty)) {  // the bucket's other two pairs and the big-table home, one round trip
+            const uint64_t h = big_home(t, key);
+            const ulonglong2 qc = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 4) & (kBucket - 2)));
+            const ulonglong2 qd = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 6) & (kBucket - 2)));
+            const unsigned long long kb = t.keys[kHotSlots + h];
+            match |= ((uint32_t)(qc.x == key) << 4) | ((uint32_t)(qc.y == key) << 5) | ((uint32_t)(qd.x == key) << 6) |
+                     ((uint32_t)(qd.y == key) << 7);
+            empty |= ((uint32_t)(qc.x == 0ull) << 4) | ((uint32_t)(qc.y == 0ull) << 5) | ((uint32_t)(qd.x == 0ull) << 6) |
+                     ((uint32_t)(qd.y == 0ull) << 7);
+            if (!(match | empty)) {  // a full bucket: the word lives in the big table
+                const uint64_t s = kHotSlots + h;
+                if (kb == key) return (uint32_t)s;
+                return kb == 0ull && table_claim(t, s, key, pos) == key ? (uint32_t)s : kSlotNone;
+            }
+        }
+        return fast ? bucket_resolve(t, match, empty, key, bbase, start, pos) : kSlotNone;
+    }
+};
+
+// K1b for the chunk of this wave (the kernel body; Probe: HotProbe or DeepProbe in the product).
 template <class Probe>
 __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                const uint64_t* __restrict__ file_start,
@@ -990,7 +1032,7 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
 // kKeysArg: the narrow chunks' key capacity comes from the argument (the
 // II_NARROW_KEYS test knob); otherwise it is the constant kNarrowKeys (the
 // SGPR-capped kernel re-read the argument from memory once per batch).
-template <bool kKeysArg>
+template <bool kKeysArg, bool kDeep>
 __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t nch,
                                                      const uint64_t* __restrict__ file_start,
                                                      uint64_t* __restrict__ chunk_off, uint64_t cap, Table tab,
@@ -1004,8 +1046,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
     // at 10 GB, same-box A/B)
     const uint64_t c = (uint64_t)blockIdx.x * kWG + w;
     if (c < nch)
-        tok_emit_chunk<HotProbe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
-                                 longs, long_per, kKeysArg ? narrow_keys : kNarrowKeys, c, s_lds[w]);
+        tok_emit_chunk<typename std::conditional<kDeep, DeepProbe, HotProbe>::type>(
+            text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf, longs, long_per,
+            kKeysArg ? narrow_keys : kNarrowKeys, c, s_lds[w]);
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)

@@ -4,8 +4,10 @@
 # tools/build_variant.sh), each under its own time limit; the first failure
 # ends the session.
 #   tools/gpu_ab.sh TAG BYTES STEPS VARIANT...   ("base" = libii.so)
+# BYTES = "-": the workload comes from $AB_ARGS instead (e.g. "--workload config5 --rank-share 0/8").
 set -o pipefail
 TAG=$1; BYTES=$2; STEPS=$3; shift 3
+if [ "$BYTES" = "-" ]; then WL="$AB_ARGS"; else WL="--bytes $BYTES"; fi
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
@@ -13,10 +15,10 @@ cd "$ROOT" || exit 1
 for v in "$@"; do
     echo "== $v"
     if [ "$v" = "base" ]; then
-        timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 2 --bytes "$BYTES" --no-cpu-baseline --io-bytes 0 \
+        timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 2 $WL --no-cpu-baseline --io-bytes 0 \
             > "$OUT/bench_$v.log" 2>&1 || exit $?
     else
-        II_LIB_VARIANT=$v timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 2 --bytes "$BYTES" \
+        II_LIB_VARIANT=$v timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 2 $WL \
             --no-cpu-baseline --io-bytes 0 > "$OUT/bench_$v.log" 2>&1 || exit $?
     fi
     tail -1 "$OUT/bench_$v.log" | python3 -c "

@@ -355,10 +355,14 @@ def test_config5_shape_vs_oracle(nf):
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
     with ii_ctypes.Index(0) as ix:
-        ix.map_host(t, off.tolist(), ids)
-        ix.reduce()
-        assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7" % nf)
-        st = ix.stats()
+        # most words overflow the hot level: the first map probes two pairs (K1c resolves the big-table
+        # words), and the next map of the context knows it and takes DeepProbe (bucket + big home)
+        for deep in (0, 1):
+            ix.map_host(t, off.tolist(), ids)
+            ix.reduce()
+            assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7, deep probe %d" % (nf, deep))
+            st = ix.stats()
+            assert st.deep_probe == deep
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
     assert st.sort_packed == (st.sort_key_bits + st.sort_id_bits - 32 <= 8)
     assert st.sort_id_bits == (nf - 1).bit_length()
