@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -328,7 +329,50 @@ static void cli_free(cli_state *c) {
     free(c->se);
 }
 
+/* II_METRICS=path (or "-" for stderr): one JSON line per run — input, wall
+ * time, counts and device phase times of the contexts that hold the output
+ * (a per-run metrics record; the reference only prints). */
+static double wall_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+static void write_metrics(const char *dest, double t0, int M, int R, int G, uint32_t nfiles, const uint64_t *sizes,
+                          ii_ctx *single, shard *sh, int err) {
+    uint64_t bytes = 0, pairs = 0, words = 0, out = 0, tokens = 0;
+    double ms_map = 0, ms_reduce = 0;
+    for (uint32_t i = 0; i < nfiles; i++) bytes += sizes[i];
+    for (int g = 0; g < (single ? 1 : G); g++) {
+        ii_ctx *c = single ? single : sh[g].ctx;
+        ii_stats st;
+        if (!c || ii_get_stats(c, &st) != II_OK) continue;
+        pairs += st.pairs; /* owners hold disjoint letters: their pairs, words and texts add up */
+        words += st.words;
+        out += st.out_bytes;
+        if (single) {
+            tokens = st.tokens;
+            ms_map = st.ms_map;
+            ms_reduce = st.ms_total - st.ms_map;
+        }
+    }
+    const double wall = wall_ms() - t0;
+    FILE *f = strcmp(dest, "-") ? fopen(dest, "a") : stderr;
+    if (!f) return;
+    fprintf(f,
+            "{\"tool\": \"ii_index\", \"ok\": %s, \"mappers\": %d, \"reducers\": %d, \"gpus\": %d, \"files\": %u, "
+            "\"bytes\": %llu, \"wall_ms\": %.3f, \"GBps_wall\": %.4f, \"pairs\": %llu, \"words\": %llu, "
+            "\"out_bytes\": %llu",
+            err ? "false" : "true", M, R, G, nfiles, (unsigned long long)bytes, wall, wall > 0 ? bytes / (wall * 1e6) : 0.0,
+            (unsigned long long)pairs, (unsigned long long)words, (unsigned long long)out);
+    if (single)
+        fprintf(f, ", \"tokens\": %llu, \"device_ms_map\": %.3f, \"device_ms_reduce\": %.3f",
+                (unsigned long long)tokens, ms_map, ms_reduce);
+    fprintf(f, "}\n");
+    if (f != stderr) fclose(f);
+}
+
 int main(int argc, char **argv) {
+    const double t0 = wall_ms();
     if (argc < 4) {
         fprintf(stderr, "Usage: %s <num_mappers> <num_reducers> <input_file_list>\n", argv[0]); /* main.c:249 */
         return -1;
@@ -448,6 +492,8 @@ int main(int argc, char **argv) {
         free(th);
         free(wa);
     }
+    const char *metrics = getenv("II_METRICS");
+    if (metrics && *metrics) write_metrics(metrics, t0, M, R, G, (uint32_t)count, sizes, single, sh, err);
     if (single) ii_close(single);
     for (int g = 0; g < G; g++) {
         if (sh[g].ctx) ii_close(sh[g].ctx);

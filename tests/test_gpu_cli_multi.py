@@ -64,3 +64,22 @@ def test_cli_owner_sort_forms(case, G, env):
     # II_IMPORT_ID_SORT=1 sorts always (u32 records), =64 sorts the u64 records — byte-identical
     got, expected, _, _ = run_cli(case, 3, 26, dict({"II_GPUS": str(G), "II_LETTER_SPLIT": "balanced"}, **env))
     assert_same(got, expected, "%s II_GPUS=%d %s" % (case, G, env))
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_cli_metrics_line(G):
+    """II_METRICS=path: the CLI appends one JSON line per run whose
+    counts agree with the output it wrote."""
+    import json
+    with tempfile.TemporaryDirectory() as md:
+        path = os.path.join(md, "m.jsonl")
+        got, expected, _, _ = run_cli("config2", 4, 26, {"II_GPUS": str(G), "II_METRICS": path})
+        assert_same(got, expected, "metrics run G=%d" % G)
+        lines = open(path).read().splitlines()
+    assert len(lines) == 1
+    m = json.loads(lines[0])
+    assert m["ok"] is True and m["gpus"] == G and m["files"] == 355 and m["bytes"] == 5756194
+    assert m["words"] == sum(v.count(b"\n") for v in expected.values())
+    assert m["pairs"] == sum(v.count(b" ") + v.count(b"\n") for v in expected.values())
+    assert m["out_bytes"] == sum(len(v) for v in expected.values())
+    assert m["wall_ms"] > 0
