@@ -514,7 +514,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
         reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
     HIPCK(hipGetLastError());
-    // two bucket-local onesweep passes: u32 -> u32 (padded), u32 -> u64 (dense)
+    // two bucket-local onesweep passes, both u32 -> u32 in the padded buckets (K3 reads that layout)
     for (int p = 0; p < 2; p++) {
         CK(lookback_pass(c, ntb * kRadix));
         const bool evp = c->n_sc < kMaxTimedPasses;
