@@ -176,14 +176,24 @@ def pmc_traffic(build):
 
 
 # the kernels of the sort + segmented-reduce phase (K2 token sort + K3), by rocprof name prefix
-PHASE_KERNELS = ("ii::k_sort0_compact", "ii::k_radix_scatter<false, 512, 16, true>", "ii::k_seg_hist",
-                 "ii::k_onesweep", "ii::k_uniq_sweep", "ii::k_radix_scatter<false, 512, 16, false>")
+# (prefixes: the template arguments that follow vary with the build, e.g. the key type)
+PHASE_KERNELS = ("ii::k_sort0_compact", "ii::k_radix_scatter<false, 512, 16, true", "ii::k_seg_hist",
+                 "ii::k_onesweep", "ii::k_uniq_sweep", "ii::k_radix_scatter<false, 512, 16, false")
+
+
+def kernel_entry(traffic, prefix):
+    """The PMC summary's entry of the kernel whose name starts with prefix (template
+    instances such as k_tok_emit<false, false> included), or {}."""
+    for k, v in traffic.items():
+        if k == prefix or k.startswith(prefix + "<"):
+            return v
+    return {}
 
 
 def pmc_phase_bytes(traffic):
     """HBM bytes per step of the phase kernels from the PMC summary (per-launch
     traffic x launches per step; a step runs k_sort0_compact once)."""
-    steps = traffic.get("ii::k_sort0_compact<true>", {}).get("dispatches_FETCH_SIZE")
+    steps = kernel_entry(traffic, "ii::k_sort0_compact").get("dispatches_FETCH_SIZE")
     if not steps:
         return None
     tot = 0.0
@@ -669,10 +679,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
                          "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(em_achieved / HBM_PEAK_GBS, 4),
-                         "traffic": round(traffic["ii::k_tok_emit"]["traffic_bytes_per_launch"])
-                         if "ii::k_tok_emit" in traffic else None,
-                         "traffic_raw": round(traffic["ii::k_tok_emit"]["traffic_raw_bytes_per_launch"])
-                         if "traffic_raw_bytes_per_launch" in traffic.get("ii::k_tok_emit", {}) else None,
+                         "traffic": round(kernel_entry(traffic, "ii::k_tok_emit")["traffic_bytes_per_launch"])
+                         if "traffic_bytes_per_launch" in kernel_entry(traffic, "ii::k_tok_emit") else None,
+                         "traffic_raw": round(kernel_entry(traffic, "ii::k_tok_emit")["traffic_raw_bytes_per_launch"])
+                         if "traffic_raw_bytes_per_launch" in kernel_entry(traffic, "ii::k_tok_emit") else None,
                          "traffic_source": traffic_src,
                          "bytes_per_launch": st.emit_bytes, "ms_per_launch": round(em_ms, 4)},
             "roofline_sort": {"bound": "hbm", "kernel": "k_radix_scatter (token sort passes)",
