@@ -157,11 +157,12 @@ def libii_sha16():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(build):
+def pmc_traffic(build, shape):
     """HBM bytes per launch by kernel from the newest committed rocprofv3 PMC
     summary (profiles/*_pmc_traffic.json, made by profiles/pmc_traffic.py from
     this same bench command), only if it was measured on this very libii.so
-    build; ({}, reason) otherwise."""
+    build and on this workload (shape = bytes, files, GPUs, rank share: a
+    kernel's traffic per launch depends on its input); ({}, reason) otherwise."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
     if not files:
@@ -170,8 +171,12 @@ def pmc_traffic(build):
         d = json.load(open(files[-1]))
     except Exception as e:  # noqa: BLE001
         return {}, "unreadable %s: %s" % (os.path.basename(files[-1]), e)
-    if d.get("bench_line", {}).get("libii_sha16") != build:
+    line = d.get("bench_line", {})
+    if line.get("libii_sha16") != build:
         return {}, "%s was measured on another libii.so build" % os.path.basename(files[-1])
+    cfg = line.get("config", {})
+    if (cfg.get("bytes"), cfg.get("files"), line.get("n_gpus"), cfg.get("rank_share")) != shape:
+        return {}, "%s was measured on another workload" % os.path.basename(files[-1])
     return ({k: v for k, v in d["kernels"].items() if "traffic_bytes_per_launch" in v}, os.path.basename(files[-1]))
 
 
@@ -519,12 +524,16 @@ def main():
 
     idx = ii_ctypes.Index(local if world > 1 else 0)
     owned = [(0, 26)]
+    local_st = [None]  # N > 1: the rank's stats after its map + local reduce (the owner's import maps again)
 
-    def step(copy_text=False):
+    def keep_local(ix):
+        local_st[0] = ix.stats()
+
+    def step(copy_text=False, capture=False):
         idx.map_device(d_text.data_ptr(), nbytes, file_start, file_ids)
         if world > 1:  # local reduce -> letter-range all-to-allv (RCCL) -> owner merge + format
             _, (lo, hi) = ii_dist.exchange_and_reduce(idx, id_bound, balanced=a.letter_split == "balanced",
-                                                      copy_text=copy_text)
+                                                      copy_text=copy_text, on_local=keep_local if capture else None)
             owned[0] = (lo[rank], hi[rank])
         else:
             idx.reduce(copy_text=copy_text)
@@ -537,17 +546,22 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     scatter_ms, emit_ms, phase_ms = [], [], []
-    for _ in range(a.steps):
-        step()
-        st = idx.stats()
-        scatter_ms.append(st.scatter_ms_avg)
-        emit_ms.append(st.emit_ms)
-        phase_ms.append(st.ms_sort + st.ms_reduce)
+    for i in range(a.steps):
+        step(capture=world > 1 and i == a.steps - 1)
+        if world == 1:
+            st = idx.stats()
+            scatter_ms.append(st.scatter_ms_avg)
+            emit_ms.append(st.emit_ms)
+            phase_ms.append(st.ms_sort + st.ms_reduce)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    st = idx.stats()
+    # the kernel figures (roofline, phases, counts) of an N > 1 line describe this rank's map + local
+    # reduce of the last timed step; after the exchange the context holds the owner's import instead
+    st = idx.stats() if world == 1 else local_st[0]
+    if world > 1:
+        scatter_ms, emit_ms, phase_ms = [st.scatter_ms_avg], [st.emit_ms], [st.ms_sort + st.ms_reduce]
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -610,7 +624,8 @@ def main():
         sc_achieved = st.scatter_bytes / (sc_ms * 1e-3) / 1e9 if sc_ms > 0 else 0.0
         em_ms = sum(emit_ms) / len(emit_ms)
         em_achieved = st.emit_bytes / (em_ms * 1e-3) / 1e9 if em_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(build)
+        traffic, traffic_src = pmc_traffic(build, (a.bytes if strong else a.bytes * world, a.files, world,
+                                                   "%d/%d" % a.share if a.share else None))
         # sort + segmented-reduce phase (K2 token sort + K3 unique), three byte counts:
         #  impl (frac, the primary figure): the bytes this build's kernels must move —
         #          the first pass reads T records (u32 / u64 as K1 wrote them, counted
@@ -707,6 +722,8 @@ def main():
             "cpu_baseline": cpu,
             "io": io,
             "e2e": e2e,
+            "kernel_figures_of": "this run" if world == 1 else
+            "rank 0's map + local reduce (last timed step; the owner's import maps again)",
             "phases_ms": {k: round(getattr(st, k), 3) for k in
                           ["ms_map", "ms_dict", "ms_sort", "ms_reduce", "ms_order", "ms_format", "ms_total",
                            "emit_ms", "resolve_ms"]},

@@ -55,13 +55,15 @@ def owner_ranges(idx_loads, world):
     return ii_ctypes.balanced_letters(total, world)
 
 
-def exchange_and_reduce(idx, id_bound, group=None, copy_text=False, balanced=False):
+def exchange_and_reduce(idx, id_bound, group=None, copy_text=False, balanced=False, on_local=None):
     """Local reduce -> export -> all-to-allv -> import -> order + format.
     After it, idx holds the final text of this rank's letters — the
     reference's reducer map ii_reducer_letters(rank, world) (main.c:129-130),
     or with balanced=True the histogram-balanced ranges every rank derives from
     the same all-reduced letter loads; the other letters are empty.  Returns
-    (recv_sizes, (letter_lo, letter_hi))."""
+    (recv_sizes, (letter_lo, letter_hi)).  on_local(idx), if given, runs once the
+    local map + reduce + export are done (before the import maps the received
+    words in the same context)."""
     import ii_ctypes
     world = dist.get_world_size(group)
     if balanced:
@@ -75,6 +77,8 @@ def exchange_and_reduce(idx, id_bound, group=None, copy_text=False, balanced=Fal
     send_off, total = prefix(sizes)
     send = torch.empty(max(total, 8), dtype=torch.uint8, device="cuda")
     idx.export(world, send.data_ptr(), send_off)
+    if on_local is not None:
+        on_local(idx)
     recv, recv_sizes = alltoallv_bytes(send[:total], sizes, group)
     recv_off, _ = prefix(recv_sizes)
     if recv.numel() == 0:
