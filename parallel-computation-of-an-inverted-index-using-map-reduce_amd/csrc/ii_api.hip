@@ -1864,16 +1864,19 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.resolved_tokens = c->n_pending;
         s.emit_bytes = c->nbytes + 8 * c->T;  // tokenize = B + r*T, r = 8-byte record
     }
-    if (c->reduced) {
+    s.deep_probe = c->map_deep ? 1u : 0u;
+    if (c->reduced || c->have_pairs) {  // (a local reduce, ii_reduce_local / the export, has these too)
         s.pairs = c->U;
-        s.out_bytes = c->out_bytes;
         s.sort_passes = c->stats.sort_passes;
         s.ms_dict = ev_ms(c->ev[1], c->ev[2]);
         s.ms_sort = ev_ms(c->ev[2], c->ev[3]);
         s.ms_reduce = ev_ms(c->ev[3], c->ev[4]);
-        s.ms_order = ev_ms(c->ev[4], c->ev[5]);
-        s.ms_format = ev_ms(c->ev[5], c->ev[6]);
-        s.ms_total = ev_ms(c->ev[0], c->ev[6]);
+        if (c->reduced) {
+            s.out_bytes = c->out_bytes;
+            s.ms_order = ev_ms(c->ev[4], c->ev[5]);
+            s.ms_format = ev_ms(c->ev[5], c->ev[6]);
+            s.ms_total = ev_ms(c->ev[0], c->ev[6]);
+        }
         double sum = 0;
         uint64_t bytes = 0;
         for (int i = 0; i < c->n_sc; i++) {
@@ -1886,7 +1889,6 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
         s.pair_bytes = c->pairs32 ? 4u : 8u;
-        s.deep_probe = c->map_deep ? 1u : 0u;
         s.sort_key_bits = (uint32_t)c->sort_W;
         s.sort_id_bits = (uint32_t)c->sort_F;
         s.sorted_records = c->T_sorted;
