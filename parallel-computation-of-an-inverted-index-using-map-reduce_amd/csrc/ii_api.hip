@@ -60,6 +60,8 @@ struct ii_ctx {
     DBuf rec, rec2, longs, pend, pend_cnt, chunk_files;
     DBuf tkeys, trep;
     uint64_t big_cap = 1ull << 22;  // big word table; total slots = kHotSlots + big_cap
+    uint64_t big_next = 0;          // big_cap for the next map, from the last local reduce's V (0: keep)
+    bool big_fixed = false;         // II_TABLE_LOG2 set the capacity (a test knob): never shrunk
     uint64_t long_cap = 0;
     uint64_t seed = 0x51ed270b27a3f3c1ull;
     // dictionary
@@ -639,7 +641,10 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     c->test_collide = getenv("II_TEST_COLLIDE") && !strcmp(getenv("II_TEST_COLLIDE"), "1");
     if (getenv("II_TEST_LONG_KEY_BITS")) c->test_long_bits = std::min(64, std::max(0, atoi(getenv("II_TEST_LONG_KEY_BITS"))));
     const char* s = getenv("II_TABLE_LOG2");
-    if (s && atoi(s) >= 10 && atoi(s) <= 30) c->big_cap = 1ull << atoi(s);
+    if (s && atoi(s) >= 10 && atoi(s) <= 30) {
+        c->big_cap = 1ull << atoi(s);
+        c->big_fixed = true;
+    }
     memset(&c->stats, 0, sizeof(c->stats));
     *out = c;
     return II_OK;
@@ -759,6 +764,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         c->mapped = true;
         return II_OK;
     }
+    // a big table sized by the last local reduce's vocabulary (shrink only): the map's memset, its
+    // occupancy count and the dictionary's slot compaction read every slot (2^22 of them: 32 MB for
+    // the 4·10^4 big-table words of configs[2])
+    if (!dense && c->big_next && c->big_next < c->big_cap && !c->big_fixed) c->big_cap = c->big_next;
     const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
     const uint32_t wg_chunks = (uint32_t)((nch + kWG - 1) / kWG);  // K1 kernels: one wave per chunk
     c->nch_map = nch;
@@ -1348,6 +1357,15 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     // the next map's probe depth: DeepProbe when most distinct words live in the big table (NW = the
     // hot slots + the big-table words; wid keys only: lexid keys leave the choice as it was)
     if (wid) c->deep_probe = 2 * (c->NW - kHotSlots) > V;
+    // the next map's big table: map_core regrows it when V > kHotSlots / 2 + big_cap / 2, so leave
+    // room for 1.5 V, and keep the big table's load under 1/4 (a power of two, at least 2^16)
+    // (input maps only: an import's vocabulary is one letter range of the shard's)
+    if (c->text_is_input) {
+        const uint64_t in_big = wid ? c->NW - kHotSlots : V;
+        uint64_t want = 1ull << 16;
+        while (kHotSlots / 2 + want / 2 < 3 * V / 2 || want < 4 * in_big) want <<= 1;
+        c->big_next = want;
+    }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     if (dict_side) {
         HIPCK(hipEventSynchronize(c->ev_dict[0]));  // (the sort's own synchronisation is past it already)

@@ -368,6 +368,24 @@ def test_config5_shape_vs_oracle(nf):
     assert st.sort_id_bits == (nf - 1).bit_length()
 
 
+def test_table_sized_by_last_vocabulary():
+    # a context's next map sizes its big table by the last local reduce's vocabulary (shrink only,
+    # ii_api.hip map_core): the second map of a small-vocabulary corpus takes a smaller table with no
+    # regrow, and a larger vocabulary after it regrows (retries) and stays exact
+    small = ii_ctypes.zipf_corpus(20_000_000, 64, 50_000, 3, threads=8)
+    large = ii_ctypes.zipf_corpus(60_000_000, 64, 4_000_000, 4, threads=8)
+    with ii_ctypes.Index(0) as ix:
+        caps = []
+        for t, off in (small, small, large):
+            ids = list(range(len(off) - 1))
+            ix.map_host(t, off.tolist(), ids)
+            ix.reduce()
+            assert_same(ix.letters(), oracle_index(t, off, ids), "table sizing, cap %d" % ix.stats().table_cap)
+            caps.append((ix.stats().table_cap, ix.stats().retries))
+    assert caps[1][0] < caps[0][0] and caps[1][1] == 0, caps
+    assert caps[2][1] >= 1, caps
+
+
 def test_large_vocab_vs_oracle_both_key_modes():
     # V ~ 2.2M distinct words (> 2^21): lexids need 22 bits, many words overflow
     # the hot level, so the word-id keys mix hot slots and big-table ranks;
