@@ -40,7 +40,9 @@ struct ii_ctx {
     bool test_collide = false;  // test knob II_TEST_COLLIDE=1: the first check of the context reports a collision
     uint32_t collide_retries = 0;
     int test_long_bits = 64;    // test knob II_TEST_LONG_KEY_BITS=b: the first map of a context hashes long words to b bits
-    uint64_t* hbuf = nullptr;   // pinned host words for readbacks queued before a later sync
+    uint64_t* hbuf = nullptr;   // pinned host words for readbacks queued before a later sync (kHbufWords):
+                                // [0] collide verdict, [1] V check, [2, 4) K3, [4, 8) MSD, [16, 64) map, [64, ) read_u64
+    hipEvent_t ev_rd = nullptr;  // after a readback queued ahead of further work (read_wait)
 
     // input
     DBuf text_own;  // text copied in by ii_map_host / ii_map_files
@@ -97,7 +99,8 @@ struct ii_ctx {
     int part_lo[II_MAX_PARTS] = {0}, part_hi[II_MAX_PARTS] = {0};  // letter range of every export part
 
     uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
-    bool test_lb_timeout = false;  // test knob II_TEST_LB_TIMEOUT: K3's timeout flag raised (its check must fail)
+    int test_lb_timeout = 0;  // test knob II_TEST_LB_TIMEOUT: the look-back timeout flag raised after K3 (1) or
+                              // after the token sort (sort: K3 must skip its work); the reduce must fail
     uint32_t retries = 0;
     bool mapped = false, have_pairs = false, reduced = false;
     uint64_t* rec_sorted = nullptr;
@@ -189,9 +192,31 @@ static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
+// Readbacks go through the pinned words c->hbuf: a copy into pageable memory is a synchronisation of its
+// own (two in a row cost two host round trips of GPU idle time).
+constexpr size_t kHbufWords = 128, kHbufRead = 64;
 static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
-    HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    if (n > kHbufWords - kHbufRead) {  // (larger tables: straight into the caller's memory)
+        HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+        HIPCK(hipStreamSynchronize(c->st));
+        return II_OK;
+    }
+    HIPCK(hipMemcpyAsync(c->hbuf + kHbufRead, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
     HIPCK(hipStreamSynchronize(c->st));
+    memcpy(out, c->hbuf + kHbufRead, n * sizeof(uint64_t));
+    return II_OK;
+}
+// A readback queued ahead of more work (read_queue ... launches ... read_wait): the host wakes while the
+// later kernels run, and what it launches next is queued behind them, so the GPU does not idle for the
+// round trip.  (hbuf words [at, at + n), at + n <= kHbufRead.)
+static int read_queue(ii_ctx* c, const void* dptr, size_t at, size_t n) {
+    HIPCK(hipMemcpyAsync(c->hbuf + at, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    HIPCK(hipEventRecord(c->ev_rd, c->st));
+    return II_OK;
+}
+static int read_wait(ii_ctx* c, uint64_t* out, size_t at, size_t n) {
+    HIPCK(hipEventSynchronize(c->ev_rd));
+    memcpy(out, c->hbuf + at, n * sizeof(uint64_t));
     return II_OK;
 }
 
@@ -481,6 +506,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);
     HIPCK(hipMemsetAsync(gh, 0, sizeof(uint64_t) * 2 * nb * kRadix, c->st));
     HIPCK(hipGetLastError());
+    CK(read_queue(c, totals + 4, 4, 4));  // (kept count, wid range: read back while the scatter runs)
     // MSD scatter: u64 records -> u32 records in padded buckets
     const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
@@ -490,7 +516,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
     uint64_t t47[4];
-    CK(read_u64(c, totals + 4, t47, 4));
+    CK(read_wait(c, t47, 4, 4));
     const uint64_t n_in = n;
     n = t47[0];
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
@@ -594,17 +620,20 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
             fmap, u32, g64);
         k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     }
+    // K3's look-back flags kLbTimeout instead of hanging (a predecessor tile that never
+    // published reads as a prefix of 0): the pairs and offsets are then wrong — an error.
+    // The flags and U are read back while k_wid_post runs.
+    uint64_t* ovf = P_<uint64_t>(c->counters) + C_OVERFLOW;
+    if (c->test_lb_timeout == 1) k_set_bits<<<1, 1, 0, c->st>>>(ovf, kLbTimeout);
+    HIPCK(hipMemcpyAsync(c->hbuf + 2, ovf, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    CK(read_queue(c, ps + c->V, 3, 1));
     if (wid)
         k_wid_post<<<grid_for(c->V), kBlock, 0, c->st>>>(P_<uint32_t>(c->widl), (uint32_t)c->V, ps_k, pe_k, ps, pe);
     HIPCK(hipGetLastError());
-    // K3's look-back flags kLbTimeout instead of hanging (a predecessor tile that never
-    // published reads as a prefix of 0): the pairs and offsets are then wrong — an error
-    uint64_t* ovf = P_<uint64_t>(c->counters) + C_OVERFLOW;
-    if (c->test_lb_timeout) k_set_bits<<<1, 1, 0, c->st>>>(ovf, kLbTimeout);
-    uint64_t flags = 0;
-    HIPCK(hipMemcpyAsync(&flags, ovf, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
-    CK(read_u64(c, ps + c->V, &c->U));
-    if (flags & kLbTimeout) return II_ERR_INTERNAL;
+    uint64_t fu[2];
+    CK(read_wait(c, fu, 2, 2));
+    c->U = fu[1];
+    if (fu[0] & kLbTimeout) return II_ERR_INTERNAL;
     HIPCK(hipMemcpyAsync(Pp + c->U, totals + 6, sizeof(uint64_t), hipMemcpyDeviceToDevice, c->st));
     return II_OK;
 }
@@ -630,14 +659,15 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     for (auto& e : c->ev_res) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_c0) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_dict) HIPCK(hipEventCreate(&e));
-    HIPCK(hipHostMalloc((void**)&c->hbuf, 64 * sizeof(uint64_t), hipHostMallocDefault));
+    HIPCK(hipHostMalloc((void**)&c->hbuf, kHbufWords * sizeof(uint64_t), hipHostMallocDefault));
+    HIPCK(hipEventCreateWithFlags(&c->ev_rd, hipEventDisableTiming));
     if (grow(c->partial, sizeof(uint64_t) * (2 * kMaxChunks + 1)) ||
         grow(c->partial2, sizeof(uint64_t) * (2 * kMaxChunks + 1)) || grow(c->totals, sizeof(uint64_t) * 16) ||
         grow(c->counters, sizeof(uint64_t) * C_NUM)) {
         ii_close(c);
         return II_ERR_NOMEM;
     }
-    c->test_lb_timeout = getenv("II_TEST_LB_TIMEOUT") && !strcmp(getenv("II_TEST_LB_TIMEOUT"), "1");
+    if (const char* e = getenv("II_TEST_LB_TIMEOUT")) c->test_lb_timeout = !strcmp(e, "1") ? 1 : !strcmp(e, "sort") ? 2 : 0;
     c->test_collide = getenv("II_TEST_COLLIDE") && !strcmp(getenv("II_TEST_COLLIDE"), "1");
     if (getenv("II_TEST_LONG_KEY_BITS")) c->test_long_bits = std::min(64, std::max(0, atoi(getenv("II_TEST_LONG_KEY_BITS"))));
     const char* s = getenv("II_TABLE_LOG2");
@@ -680,6 +710,7 @@ extern "C" void ii_close(ii_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_dict)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_rd) (void)hipEventDestroy(c->ev_rd);
     if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->st2) (void)hipStreamDestroy(c->st2);
     if (c->hbuf) (void)hipHostFree(c->hbuf);
@@ -841,11 +872,13 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
             HIPCK(hipEventRecord(c->ev_res[1], c->st));
         }
         if (c->rec_cap) CK(run_scan(c, OpInPlace{chunk_cnt}, nch + 1, totals));  // chunk token counts -> voff
-        k_hist_reduce<<<kHistBlocks, kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
+        k_hist_reduce<<<hist_blocks(nch), kBlock, 0, c->st>>>(P_<uint32_t>(c->chunk_hist), nch, counters);
         HIPCK(hipGetLastError());
         uint64_t cnt[C_LONGMAX + 1], tot[10];  // (C_HIST .. C_HIST + 25 lie inside)
-        HIPCK(hipMemcpyAsync(cnt, counters, sizeof(cnt), hipMemcpyDeviceToHost, c->st));
-        CK(read_u64(c, totals, tot, 10));
+        static_assert(16 + C_LONGMAX + 1 <= kHbufRead, "map readback words");
+        HIPCK(hipMemcpyAsync(c->hbuf + 16, counters, sizeof(cnt), hipMemcpyDeviceToHost, c->st));
+        CK(read_u64(c, totals, tot, 10));  // (one synchronisation for both)
+        memcpy(cnt, c->hbuf + 16, sizeof(cnt));
         if (tot[9]) return II_ERR_LAYOUT;
         if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] > kHotSlots / 2 + c->big_cap / 2) {
             c->big_cap *= 4;
@@ -1378,11 +1411,9 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
         }
         HIPCK(hipStreamWaitEvent(c->st, c->ev_dict[1], 0));
     }
-    {
-        uint64_t ovf;
-        CK(read_u64(c, P_<uint64_t>(c->counters) + C_OVERFLOW, &ovf));
-        if (ovf & kLbTimeout) return II_ERR_INTERNAL;  // a onesweep look-back never resolved
-    }
+    // (a onesweep look-back that never resolved flags kLbTimeout: K3 then does nothing and run_unique,
+    // which reads the flags with U, returns II_ERR_INTERNAL)
+    if (c->test_lb_timeout == 2) k_set_bits<<<1, 1, 0, c->st>>>(P_<uint64_t>(c->counters) + C_OVERFLOW, kLbTimeout);
 
     // ---- K3: unique (word, file) pairs, posting byte offsets, posting starts.  The verdict of
     // the map's exactness check (k_long_verify on the side stream, map_core) is read with K3's

@@ -1051,22 +1051,37 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
             kKeysArg ? narrow_keys : kNarrowKeys, c, s_lds[w]);
 }
 
-// counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l] (one block per letter)
-// Per-letter totals of the per-chunk letter counts (chunk_hist[c * 26 + l]).
-// kHistThreads is a multiple of 26, so every thread strides over one letter's
-// column (coalesced across the grid), then one LDS and one global add per
-// letter and workgroup; counters[C_HIST ..] must be zero on entry.
-constexpr uint32_t kHistBlocks = 416;  // 416 * 256 = 26 * 4096 threads
+// counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l]: the
+// per-letter totals of the per-chunk letter counts (chunk_hist[c * 26 + l]).
+// The grid is a multiple of 13 blocks (256 · 13 threads = 26 · 128), so every
+// thread strides over one letter's column (coalesced across the grid), four
+// loads in flight; then one LDS and one global add per letter and workgroup;
+// counters[C_HIST ..] must be zero on entry.  (416 blocks with one load in
+// flight: 64 us for the 63 MB of configs[2]'s 6·10^5 chunks, on the map's
+// critical path.)
+constexpr uint32_t kHistBlocksMax = 13 * 128;
+inline uint32_t hist_blocks(uint64_t nch) {
+    const uint64_t want = (nch * 26 + 16 * kBlock - 1) / (16 * kBlock);  // ~16 loads per thread
+    const uint64_t b = (want + 12) / 13 * 13;
+    return (uint32_t)(b < 13 ? 13 : b > kHistBlocksMax ? kHistBlocksMax : b);
+}
 __global__ __launch_bounds__(kBlock) void k_hist_reduce(const uint32_t* __restrict__ chunk_hist, uint64_t nch,
                                                         uint64_t* __restrict__ counters) {
     __shared__ unsigned long long s[26];
     if (threadIdx.x < 26) s[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)kHistBlocks * kBlock, n = nch * 26;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock, n = nch * 26;
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    uint64_t acc = 0;
-    for (uint64_t e = g; e < n; e += stride) acc += chunk_hist[e];
-    atomicAdd(&s[g % 26], (unsigned long long)acc);
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint64_t e = g;
+    for (; e + 3 * stride < n; e += 4 * stride) {
+        a0 += chunk_hist[e];
+        a1 += chunk_hist[e + stride];
+        a2 += chunk_hist[e + 2 * stride];
+        a3 += chunk_hist[e + 3 * stride];
+    }
+    for (; e < n; e += stride) a0 += chunk_hist[e];
+    atomicAdd(&s[g % 26], (unsigned long long)(a0 + a1 + a2 + a3));
     __syncthreads();
     if (threadIdx.x < 26) atomicAdd((unsigned long long*)&counters[C_HIST + threadIdx.x], s[threadIdx.x]);
 }
@@ -1728,8 +1743,16 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
     __shared__ uint32_t s_tile;
     constexpr int kPer = kUniqSweepTile / kBlock;
     const int t = threadIdx.x;
-    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+    // a sort pass before this one that flagged kLbTimeout left records out of place (their keys may
+    // lie past the word range): every workgroup leaves before its ticket, and the host, which reads
+    // the flags with U, returns II_ERR_INTERNAL.  (The flag's load is in flight with the ticket.)
+    if (t == 0) {
+        const unsigned long long e0 = *err;
+        const uint32_t tk = atomicAdd(ticket, 1u);
+        s_tile = (e0 & kLbTimeout) ? ~0u : tk;
+    }
     __syncthreads();
+    if (s_tile == ~0u) return;
     const uint64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
     const uint64_t lo = tile * kUniqSweepTile;
     uint64_t ntiles, hi, first = 0, vend = 0;

@@ -487,12 +487,15 @@ def test_tiny_shapes_logical_shards(k):
     assert_same(shard_and_merge(text, off, 3), exp, "tiny %d G=3" % k)
 
 
-def test_k3_lookback_timeout_is_an_error():
-    """K3 flags a look-back that never resolved (kLbTimeout) instead of
-    hanging; the host must turn the flag into II_ERR_INTERNAL, not return the
-    wrong pairs (II_TEST_LB_TIMEOUT=1 raises the flag after K3)."""
+@pytest.mark.parametrize("where", ["1", "sort"])
+def test_k3_lookback_timeout_is_an_error(where):
+    """K3 and the onesweep passes flag a look-back that never resolved
+    (kLbTimeout) instead of hanging; the host must turn the flag into
+    II_ERR_INTERNAL, not return the wrong pairs (II_TEST_LB_TIMEOUT=1 raises
+    the flag after K3; =sort after the token sort, where K3 must skip its work:
+    the records are out of place and their keys may lie past the word range)."""
     text, off, ids, _ = case_arrays("config2")
-    os.environ["II_TEST_LB_TIMEOUT"] = "1"
+    os.environ["II_TEST_LB_TIMEOUT"] = where
     try:
         with ii_ctypes.Index(0) as ix:
             ix.map_host(text, off, ids)
