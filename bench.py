@@ -253,7 +253,17 @@ def cpu_baseline(a, text, off, runs=5):
     cores = host_cores()
     ref = os.path.join(REPO, "oracle", "_ref", "tema1")
     asan = os.path.join(REPO, "oracle", "_ref", "tema1_asan")
-    out = {"unit": "GB/s", "cores": cores, "host_cpus": os.cpu_count()}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    # BASELINE.md asks for M = nproc: nproc here counts the whole machine's CPUs (256 on the GPU box),
+    # of which one single-GPU job is granted a share — the box exports it as OMP_NUM_THREADS (16).
+    # M and the restatement's threads use that share; the reference's map phase does not scale with M
+    # anyway (shared-FILE locks) and its R is capped by the 26 letters.
+    out = {"unit": "GB/s", "cores": cores, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+           "cores_basis": "threads granted to this job (OMP_NUM_THREADS, the box's per-GPU CPU share); "
+                          "nproc counts the whole machine"}
     sl_files, sl_bytes = 360, 360 * 1000 * a.cpu_slice_kb
     st, so = ii_ctypes.zipf_corpus(sl_bytes, sl_files, a.vocab, a.seed + 77, threads=min(8, cores))
     m_ok = safe_mappers([int(so[f + 1] - so[f]) for f in range(sl_files)], cores)
@@ -376,7 +386,7 @@ def config2_lane(idx, runs=5):
             buf += d + b"\n"
         n = len(buf)
         d_text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-        d_text[:n].copy_(torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8)))
+        d_text[:n].copy_(torch.frombuffer(buf, dtype=torch.uint8))  # (a bytearray: writable, no copy)
         fs = np.asarray(starts, dtype=np.uint64)
         ids = np.arange(len(paths), dtype=np.uint32)
         ts = []

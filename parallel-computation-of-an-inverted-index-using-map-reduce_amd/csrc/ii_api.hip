@@ -17,6 +17,7 @@
 #include "../../include/ii.h"
 #include "ii_kernels.h"
 #include "ii_partial.h"
+#include "ii_reader.h"
 
 
 using namespace ii;
@@ -140,14 +141,46 @@ struct ii_ctx {
     ii_stats stats;
 };
 
+// A sticky device error (a kernel's illegal memory access, an abort, a lost
+// device) leaves every queue of the process unusable: after it, a wait on an
+// event or a stream of ANY context may never return (round 3: a CLI with
+// eight contexts on one device sat in such waits after the first context's
+// copy reported the fault).  The first sticky error poisons the library: every
+// later entry point returns II_ERR_HIP at once, with no HIP call, and
+// ii_close releases nothing on the device (the process is expected to exit).
+static volatile int g_poisoned = 0;
+static void note_hip_error(hipError_t e) {
+    switch (e) {
+        case hipErrorIllegalAddress:
+        case hipErrorLaunchFailure:
+        case hipErrorAssert:
+        case hipErrorLaunchTimeOut:
+        case hipErrorECCNotCorrectable:
+        case hipErrorNoDevice:
+        case hipErrorContextIsDestroyed:
+            __atomic_store_n(&g_poisoned, 1, __ATOMIC_SEQ_CST);
+            break;
+        default:
+            break;
+    }
+}
+static inline bool poisoned() { return __atomic_load_n(&g_poisoned, __ATOMIC_SEQ_CST) != 0; }
+
 #define HIPCK(x)                                                                               \
     do {                                                                                       \
         hipError_t e_ = (x);                                                                   \
         if (e_ != hipSuccess) {                                                                \
+            note_hip_error(e_);                                                                \
             fprintf(stderr, "libii: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
                     __LINE__);                                                                 \
             return II_ERR_HIP;                                                                 \
         }                                                                                      \
+    } while (0)
+
+// entry-point guard: no HIP call after a sticky error
+#define LIVE_OR_FAIL()                   \
+    do {                                 \
+        if (poisoned()) return II_ERR_HIP; \
     } while (0)
 
 #define CK(x)                   \
@@ -569,6 +602,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
 static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed, const uint32_t* fmap,
                       bool compact) {
     c->xpairs = false;
+    if (compact && c->id_bound > kPairFirst) compact = false;  // (the top bit marks a word's first pair: u64 pairs)
     c->pairs32 = compact;
     CK(grow(c->uniq, sizeof(uint64_t) * std::max<uint64_t>(n, 1)));
     CK(grow(c->P, sizeof(uint64_t) * (n + 1)));
@@ -582,7 +616,6 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
     uint32_t* u32 = nullptr;
     uint32_t* g64 = nullptr;
     if (compact) {  // (file ids below 2^31: the top bit marks a word's first pair)
-        if (c->id_bound > kPairFirst) return II_ERR_ARG;
         CK(grow(c->g64, sizeof(uint32_t) * (n / 64 + 2)));
         u32 = P_<uint32_t>(c->uniq);
         g64 = P_<uint32_t>(c->g64);
@@ -590,6 +623,9 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
     if (n == 0) {
         HIPCK(hipMemsetAsync(ps + c->V, 0, sizeof(uint64_t), c->st));
         HIPCK(hipMemsetAsync(Pp, 0, sizeof(uint64_t), c->st));
+        // (the callers read host words queued on the stream before this call — local_reduce's
+        // collision verdict — after run_unique returns: the other path's read_wait covers them)
+        HIPCK(hipStreamSynchronize(c->st));
         c->U = 0;
         return II_OK;
     }
@@ -642,6 +678,7 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
 extern "C" int ii_open(ii_ctx** out, int device) {
     if (!out) return II_ERR_ARG;
     *out = nullptr;
+    LIVE_OR_FAIL();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
         (void)hipGetLastError();
@@ -682,6 +719,10 @@ extern "C" int ii_open(ii_ctx** out, int device) {
 
 extern "C" void ii_close(ii_ctx* c) {
     if (!c) return;
+    if (poisoned()) {  // (a wait or free on a faulted device may never return: leave it to process exit)
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->st2) (void)hipStreamSynchronize(c->st2);  // (work on st2 reads the buffers freed below)
@@ -924,6 +965,16 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     return II_OK;
 }
 
+// A map's exactness check (k_long_verify on st2) still reads c->text, the
+// word table and the long queue until the reduce reads its verdict.  A new
+// map before that reduce must not overwrite the text under it (ii_map_host /
+// ii_map_files / ii_import write text_own from the host or the io streams
+// before map_core orders c->st behind the check): wait for it on the host.
+static int settle_side(ii_ctx* c) {
+    if (c->lv_pending) HIPCK(hipEventSynchronize(c->ev_res[1]));
+    return II_OK;
+}
+
 static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file_id0, uint32_t nfiles) {
     for (uint32_t f = 1; f < nfiles; f++)
         if (file_id0[f] <= file_id0[f - 1] || file_start[f] < file_start[f - 1]) return II_ERR_ARG;
@@ -955,7 +1006,9 @@ extern "C" int ii_map_device(ii_ctx* c, const uint8_t* d_text, uint64_t nbytes, 
                              const uint32_t* file_id0, uint32_t nfiles, uint64_t hist_out[II_ALPHABET]) {
     if (!c || (nfiles && (!file_start || !file_id0)) || (nbytes && !d_text)) return II_ERR_ARG;
     if (((uintptr_t)d_text & 15u) != 0) return II_ERR_ARG;  // 16-byte staging loads
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
+    CK(settle_side(c));
     c->text = d_text;
     c->nbytes = nbytes;
     CK(set_files(c, file_start, file_id0, nfiles));
@@ -969,7 +1022,9 @@ static bool host_ws(uint8_t ch) { return ch == ' ' || (ch >= 9 && ch <= 13); }
 extern "C" int ii_map_host(ii_ctx* c, const uint8_t* text, const uint64_t* file_off, const uint32_t* file_id0,
                            uint32_t nfiles, uint64_t hist_out[II_ALPHABET]) {
     if (!c || (nfiles && (!file_off || !file_id0 || !text))) return II_ERR_ARG;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
+    CK(settle_side(c));
     c->io_ms = 0;
     c->io_bytes = 0;
     for (uint32_t f = 0; f < nfiles; f++)
@@ -1011,58 +1066,16 @@ constexpr int kIoThreads = 16;
 
 struct IoJob {
     ii_ctx* c;
-    const ii_file* files;
-    uint32_t nfiles;
-    const uint64_t* off;  // nfiles + 1: device offset of every file (+1 separator each)
+    IoLayout lay;  // the device layout and its host-only reader (ii_reader.h)
     uint8_t* d_text;
     uint64_t total, nwin;
     int nt;
     int err;      // first error (II_*), 0 = ok
-    int grown;    // some file had more bytes than its stat size
-    pthread_mutex_t mu;
 };
 struct IoArg {
     IoJob* j;
     int t;
 };
-
-// Fill window [lo, hi) of the device layout into buf.
-static void io_fill(IoJob* j, uint64_t lo, uint64_t hi, uint8_t* buf) {
-    uint32_t f = (uint32_t)(std::upper_bound(j->off, j->off + j->nfiles + 1, lo) - j->off) - 1;
-    for (; f < j->nfiles && j->off[f] < hi; f++) {
-        const uint64_t fsz = j->off[f + 1] - j->off[f] - 1;  // bytes of file f (separator excluded)
-        const uint64_t a = std::max(lo, j->off[f]), b = std::min(hi, j->off[f] + fsz);
-        if (b > a || (fsz == 0 && j->off[f] >= lo)) {
-            // every window that holds file bytes (or the separator of an empty file) opens it;
-            // only the window holding the file's first byte reports a failure (main.c:98)
-            const int fd = open(j->files[f].path, O_RDONLY);
-            const bool first = j->off[f] >= lo;
-            if (fd < 0) {
-                if (first) fprintf(stderr, "Mapper %d: Error opening file %s\n", j->files[f].mapper, j->files[f].path);
-                if (b > a) memset(buf + (a - lo), ' ', b - a);
-            } else {
-                uint64_t done = 0;
-                while (a + done < b) {
-                    const ssize_t r = pread(fd, buf + (a + done - lo), b - a - done, (off_t)(a + done - j->off[f]));
-                    if (r <= 0) break;
-                    done += (uint64_t)r;
-                }
-                if (a + done < b) memset(buf + (a + done - lo), ' ', b - a - done);  // shorter than stat: spaces
-                if (j->off[f] + fsz <= hi) {  // this window holds the file's end: is there more?
-                    uint8_t extra;
-                    if (pread(fd, &extra, 1, (off_t)fsz) == 1) {
-                        pthread_mutex_lock(&j->mu);
-                        j->grown = 1;
-                        pthread_mutex_unlock(&j->mu);
-                    }
-                }
-                close(fd);
-            }
-        }
-        const uint64_t sep = j->off[f] + fsz;  // separator byte of file f
-        if (sep >= lo && sep < hi) buf[sep - lo] = '\n';
-    }
-}
 
 static void* io_worker(void* p) {
     IoArg* a = (IoArg*)p;
@@ -1075,16 +1088,16 @@ static void* io_worker(void* p) {
         const int b = 2 * a->t + k;
         if (hipEventSynchronize(c->io_ev[b]) != hipSuccess) { err = II_ERR_HIP; break; }  // buffer free again
         const uint64_t lo = w * kIoWin, hi = std::min(j->total, lo + kIoWin);
-        io_fill(j, lo, hi, c->io_buf[b]);
+        io_fill(&j->lay, lo, hi, c->io_buf[b]);
         if (hipMemcpyAsync(j->d_text + lo, c->io_buf[b], hi - lo, hipMemcpyHostToDevice, c->io_st[a->t]) != hipSuccess ||
             hipEventRecord(c->io_ev[b], c->io_st[a->t]) != hipSuccess)
             err = II_ERR_HIP;
     }
     if (err == II_OK && hipStreamSynchronize(c->io_st[a->t]) != hipSuccess) err = II_ERR_HIP;
     if (err != II_OK) {
-        pthread_mutex_lock(&j->mu);
+        pthread_mutex_lock(&j->lay.mu);
         if (!j->err) j->err = err;
-        pthread_mutex_unlock(&j->mu);
+        pthread_mutex_unlock(&j->lay.mu);
     }
     return nullptr;
 }
@@ -1166,7 +1179,9 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
     if (!c || (nfiles && !files)) return II_ERR_ARG;
     for (uint32_t f = 0; f < nfiles; f++)
         if (!files[f].path || (f && files[f].id0 <= files[f - 1].id0)) return II_ERR_ARG;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
+    CK(settle_side(c));
     const double t0 = now_ms();
     std::vector<uint64_t> off(nfiles + 1, 0);
     for (uint32_t f = 0; f < nfiles; f++) off[f + 1] = off[f] + files[f].size + 1;
@@ -1175,8 +1190,8 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
     const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nthreads, 1), (uint64_t)kIoThreads,
                                                                     (total + kIoWin - 1) / kIoWin}));
     CK(io_setup(c, nt));
-    IoJob job{c, files, nfiles, off.data(), P_<uint8_t>(c->text_own), total, (total + kIoWin - 1) / kIoWin, nt, 0, 0,
-              PTHREAD_MUTEX_INITIALIZER};
+    IoJob job{c, IoLayout{files, nfiles, off.data(), 0, PTHREAD_MUTEX_INITIALIZER}, P_<uint8_t>(c->text_own), total,
+              (total + kIoWin - 1) / kIoWin, nt, 0};
     std::vector<pthread_t> th(nt);
     std::vector<IoArg> args(nt);
     for (int t = 0; t < nt; t++) {
@@ -1185,7 +1200,7 @@ extern "C" int ii_map_files(ii_ctx* c, const ii_file* files, uint32_t nfiles, in
     }
     for (int t = 0; t < nt; t++) pthread_join(th[t], nullptr);
     if (job.err) return job.err;
-    if (job.grown) return read_all_then_map(c, files, nfiles, nthreads, hist_out);
+    if (job.lay.grown) return read_all_then_map(c, files, nfiles, nthreads, hist_out);
     c->io_ms = now_ms() - t0;
     c->io_bytes = total;
     c->text = P_<uint8_t>(c->text_own);
@@ -1521,18 +1536,32 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     return II_OK;
 }
 
+// The exchange needs the u64 (word, id0) pairs of a word-id reduce.  A
+// formatted-only reduce (ii_reduce) wrote compact pairs and its token sort
+// consumed the K1 records in place (the packed passes write u32 records into
+// rec), so an export after it maps the same input again before the local
+// reduce (the input is the context's own copy, or the caller's d_text, which
+// the context keeps until the next map call).  An owner's merged pairs
+// (ii_import) are not exported again.
+static int exportable_pairs(ii_ctx* c) {
+    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;
+    if (c->have_pairs && !c->pairs32) return II_OK;
+    if (c->have_pairs && c->pairs32) CK(map_core(c, nullptr));  // records consumed: map again
+    return local_reduce(c, true, false);
+}
+
 extern "C" int ii_reduce_local(ii_ctx* c) {
     if (!c) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
-    if (c->have_pairs && !c->pairs32) return II_OK;
-    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;  // an owner's merged pairs are not exported again
-    return local_reduce(c, true, false);
+    return exportable_pairs(c);
 }
 
 extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
     if (!c) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
     if (!c->have_pairs) CK(local_reduce(c, true, true));  // formatted only: compact pairs
     return order_and_format(c, copy_text);
@@ -1596,9 +1625,9 @@ static int plan_core(ii_ctx* c, int nparts, const int* lo_in, const int* hi_in, 
         c->part_hi[r] = hi;
     }
     if (c->part_hi[nparts - 1] != II_ALPHABET) return II_ERR_ARG;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
-    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;
-    if (!c->have_pairs || c->pairs32) CK(local_reduce(c, true, false));  // the exchange needs the u64 pairs
+    CK(exportable_pairs(c));
     CK(letter_points(c));
     for (int r = 0; r < nparts; r++) {
         const uint64_t* a = c->h_pts + 3 * c->part_lo[r];
@@ -1622,9 +1651,9 @@ extern "C" int ii_export_plan_ranges(ii_ctx* c, int nparts, const int* letter_lo
 extern "C" int ii_letter_load(ii_ctx* c, uint64_t pairs[II_ALPHABET]) {
     if (!c || !pairs) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
-    if (c->pairs32 && !c->text_is_input) return II_ERR_STATE;
-    if (!c->have_pairs || c->pairs32) CK(local_reduce(c, true, false));  // the exchange needs the u64 pairs
+    CK(exportable_pairs(c));
     CK(letter_points(c));
     for (int l = 0; l < II_ALPHABET; l++) pairs[l] = c->h_pts[3 * (l + 1) + 1] - c->h_pts[3 * l + 1];
     return II_OK;
@@ -1633,6 +1662,7 @@ extern "C" int ii_letter_load(ii_ctx* c, uint64_t pairs[II_ALPHABET]) {
 extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* send_off) {
     if (!c || nparts < 1 || !d_send || !send_off) return II_ERR_ARG;
     if (c->planned_parts != nparts) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
     for (int r = 0; r < nparts; r++) {
         if (send_off[r] & 7) return II_ERR_ARG;
@@ -1662,7 +1692,9 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
 
 extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64_t* recv_off, uint32_t id_bound) {
     if (!c || nparts < 1 || !recv_off || (!d_recv && nparts)) return II_ERR_ARG;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
+    CK(settle_side(c));
     std::vector<uint64_t> hdr(8 * (size_t)nparts);
     for (int s = 0; s < nparts; s++) {
         if (recv_off[s] & 7) return II_ERR_ARG;
@@ -1827,6 +1859,7 @@ extern "C" int ii_letter_text(ii_ctx* c, int letter, const char** buf, size_t* l
 extern "C" int ii_partials(ii_ctx* c, const uint32_t* order, uint32_t n) {
     if (!c || (n && !order)) return II_ERR_ARG;
     if (!c->mapped || !c->text_is_input) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
     c->part_valid = false;
     std::vector<PartPiece> pieces;
@@ -1897,6 +1930,7 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
 extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
     if (!c || !o) return II_ERR_ARG;
     if (!c->mapped) return II_ERR_STATE;
+    LIVE_OR_FAIL();
     ii_stats s;
     memset(&s, 0, sizeof(s));
     s.bytes = c->nbytes;

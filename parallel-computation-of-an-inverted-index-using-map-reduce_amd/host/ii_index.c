@@ -35,6 +35,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -59,19 +60,92 @@ typedef struct {
     hipStream_t st;
 } shard;
 
-/* ---- phase bodies, one pthread per context */
-static void *map_body(void *p) {
-    shard *s = p;
+/* ---- phases: one pthread per context, joined by run_phase.
+ * A failed context ends the phase at once: run_phase returns its error
+ * without waiting for the other contexts, because after a device fault their
+ * threads may sit in HIP waits that never return (round 3: eight contexts on
+ * one device, the first one's copy reported an illegal memory access, and the
+ * CLI waited for the others until it was killed).  main() then prints the
+ * error and leaves with _exit, making no further HIP call.
+ * Test knob II_TEST_FAIL=<phase>:<g> (phase map or merge): context g returns
+ * II_ERR_INTERNAL at the start of that phase and every other context of the
+ * phase blocks for good, as behind a faulted device. */
+typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int done, err;
+} phase_sync;
+
+typedef struct {
+    shard *s;
+    int g;
+    phase_sync *ps;
+    void (*body)(shard *);
+    const char *name;
+} phase_arg;
+
+static int test_fail_ctx(const char *phase) {
+    const char *e = getenv("II_TEST_FAIL");
+    size_t n = strlen(phase);
+    if (!e || strncmp(e, phase, n) || e[n] != ':') return -1;
+    return atoi(e + n + 1);
+}
+
+static void *phase_thread(void *p) {
+    phase_arg *a = p;
+    const int fail = test_fail_ctx(a->name);
+    if (fail == a->g) {
+        a->s->rc = II_ERR_INTERNAL;
+    } else if (fail >= 0) {
+        for (;;) pause(); /* the simulated stuck context */
+    } else {
+        a->body(a->s);
+    }
+    pthread_mutex_lock(&a->ps->mu);
+    a->ps->done++;
+    if (a->s->rc != II_OK && a->ps->err == II_OK) a->ps->err = a->s->rc;
+    pthread_cond_signal(&a->ps->cv);
+    pthread_mutex_unlock(&a->ps->mu);
+    return NULL;
+}
+
+/* Run body on every context; II_OK once all succeeded (threads joined), or the
+ * first error as soon as it is reported (the other threads are left alone). */
+static int run_phase(shard *sh, int G, void (*body)(shard *), const char *name) {
+    static phase_sync ps;
+    static phase_arg args[MAXG];
+    pthread_t th[MAXG];
+    pthread_mutex_init(&ps.mu, NULL);
+    pthread_cond_init(&ps.cv, NULL);
+    ps.done = 0;
+    ps.err = II_OK;
+    int started = 0;
+    for (int g = 0; g < G; g++) {
+        args[g] = (phase_arg){&sh[g], g, &ps, body, name};
+        if (pthread_create(&th[g], NULL, phase_thread, &args[g]) != 0) {
+            sh[g].rc = II_ERR_NOMEM;
+            break;
+        }
+        started++;
+    }
+    pthread_mutex_lock(&ps.mu);
+    while (ps.done < started && ps.err == II_OK) pthread_cond_wait(&ps.cv, &ps.mu);
+    int rc = ps.err;
+    pthread_mutex_unlock(&ps.mu);
+    if (rc == II_OK && started < G) rc = II_ERR_NOMEM;
+    if (rc != II_OK) return rc; /* (threads still running are not joined) */
+    for (int g = 0; g < started; g++) pthread_join(th[g], NULL);
+    return II_OK;
+}
+
+static void map_body(shard *s) {
     s->rc = ii_open(&s->ctx, s->dev);
     if (s->rc == II_OK) s->rc = ii_map_files(s->ctx, s->files, s->n, s->nthreads, NULL);
     if (s->rc == II_OK) s->rc = ii_reduce_local(s->ctx); /* lexid-keyed partial index, letter-contiguous */
-    return NULL;
 }
-static void *merge_body(void *p) {
-    shard *s = p;
+static void merge_body(shard *s) {
     s->rc = ii_import(s->ctx, s->nparts, s->d_recv, s->recv_off, s->id_bound);
     if (s->rc == II_OK) s->rc = ii_reduce(s->ctx, 1);
-    return NULL;
 }
 
 typedef struct {
@@ -163,7 +237,10 @@ static int exchange(shard *sh, int G, int distinct) {
  * local reduce every shard (one pthread per context). */
 static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count, int M, int G, shard *sh) {
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        if (test_fail_ctx("map") < 0) return II_ERR_NODEV;
+        ndev = 1; /* (the test knob's map phase opens no device: it runs without one) */
+    }
     uint32_t *order = calloc((size_t)count + 1, sizeof(uint32_t));
     uint32_t *shard_of = calloc((size_t)count + 1, sizeof(uint32_t));
     uint32_t sb[MAXG], se[MAXG];
@@ -191,14 +268,7 @@ static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count
         }
     free(order);
     free(shard_of);
-    int rc = II_OK;
-    pthread_t th[MAXG];
-    for (int g = 0; g < G; g++) pthread_create(&th[g], NULL, map_body, &sh[g]);
-    for (int g = 0; g < G; g++) {
-        pthread_join(th[g], NULL);
-        if (sh[g].rc != II_OK && rc == II_OK) rc = sh[g].rc;
-    }
-    return rc;
+    return run_phase(sh, G, map_body, "map");
 }
 
 /* Second half: letter owners, export, exchange, merge, order + format.
@@ -209,7 +279,6 @@ static int multi_exchange_body(int G, shard *sh, ii_ctx **owner) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
     const int distinct = ndev >= G;
     int rc = II_OK;
-    pthread_t th[MAXG];
 
     /* letter owners */
     int lo[MAXG], hi[MAXG];
@@ -247,16 +316,12 @@ static int multi_exchange_body(int G, shard *sh, ii_ctx **owner) {
     if ((rc = exchange(sh, G, distinct)) != II_OK) return rc;
 
     /* owners: merge the received segments, order + format (one thread per context) */
-    for (int g = 0; g < G; g++) pthread_create(&th[g], NULL, merge_body, &sh[g]);
-    for (int g = 0; g < G; g++) {
-        pthread_join(th[g], NULL);
-        if (sh[g].rc != II_OK && rc == II_OK) rc = sh[g].rc;
-    }
-    return rc;
+    return run_phase(sh, G, merge_body, "merge");
 }
 
 static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
     const int rc = multi_exchange_body(G, sh, owner);
+    if (rc != II_OK) return rc; /* (no HIP call after a failure: main() exits) */
     for (int g = 0; g < G; g++) {
         (void)hipSetDevice(sh[g].dev);
         if (sh[g].d_send) (void)hipFree(sh[g].d_send);
@@ -342,7 +407,7 @@ static void write_metrics(const char *dest, double t0, int M, int R, int G, uint
     uint64_t bytes = 0, pairs = 0, words = 0, out = 0, tokens = 0;
     double ms_map = 0, ms_reduce = 0;
     for (uint32_t i = 0; i < nfiles; i++) bytes += sizes[i];
-    for (int g = 0; g < (single ? 1 : G); g++) {
+    for (int g = 0; g < (single ? 1 : sh ? G : 0); g++) {
         ii_ctx *c = single ? single : sh[g].ctx;
         ii_stats st;
         if (!c || ii_get_stats(c, &st) != II_OK) continue;
@@ -476,8 +541,14 @@ int main(int argc, char **argv) {
     }
     int err = 0;
     if (rc != II_OK) {
+        /* a failed phase: report and leave at once — other contexts' threads may still sit in HIP
+         * calls on a faulted device, so no join, no ii_close, no device statistics */
         if (!reported) fprintf(stderr, "ii_index: %s\n", ii_strerror(rc));
-        err = 1;
+        const char *metrics = getenv("II_METRICS");
+        if (metrics && *metrics) write_metrics(metrics, t0, M, R, G, (uint32_t)count, sizes, NULL, NULL, 1);
+        fflush(stdout);
+        fflush(stderr);
+        _exit(1);
     } else if (R > 0) {
         pthread_t *th = calloc((size_t)R, sizeof(pthread_t));
         writer_arg *wa = calloc((size_t)R, sizeof(writer_arg));

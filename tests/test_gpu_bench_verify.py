@@ -26,9 +26,11 @@ def share_ids(p, rank, world):
 
 @pytest.mark.parametrize("name", ["config3", "config5share", "config5/share0of8"])
 def test_full_size_index_matches_oracle(name):
-    """config5/share0of8: rank 0's share of configs[4] over 8 GPUs (1.25*10^5
-    files whose global ids span [0, 10^6)) — the shape a real rank indexes; its
-    records carry 17-bit shard-local file indices, so the packed sort runs."""
+    """config5/share<r>of8: rank r's ii_partition share of configs[4] over 8
+    GPUs (main.c:300-323 with M = 8), with the files' GLOBAL ids in [0, 10^6)
+    — the shape a real rank indexes.  Rank 0 holds the 15 835 largest files
+    (14-bit shard-local file indices), rank 7 the 439 993 smallest (19-bit
+    indices: the widest sort keys of the job)."""
     import torch
     if name not in DB:
         pytest.skip("no oracle hashes for %s" % name)

@@ -83,3 +83,22 @@ def test_cli_metrics_line(G):
     assert m["pairs"] == sum(v.count(b" ") + v.count(b"\n") for v in expected.values())
     assert m["out_bytes"] == sum(len(v) for v in expected.values())
     assert m["wall_ms"] > 0
+
+
+def test_cli_failed_owner_exits_promptly():
+    """II_TEST_FAIL=merge:3 with II_GPUS=5: owner 3's import fails and the other
+    owners' threads block, as behind a faulted device (round 3's post-fault
+    hang): the CLI must report the error and exit non-zero within
+    15 s, making no further HIP call."""
+    import time
+    with tempfile.TemporaryDirectory() as td:
+        materialize("config2", td)
+        env = dict(os.environ, II_GPUS="5", II_TEST_FAIL="merge:3")
+        t0 = time.time()
+        r = subprocess.run([os.path.join(PKG, "ii_index"), "3", "26", "list.txt"], cwd=td, capture_output=True,
+                           timeout=120, env=env)
+        dt = time.time() - t0
+    err = r.stderr.decode(errors="replace")
+    assert r.returncode == 1, err
+    assert "internal consistency check failed" in err, err
+    assert dt < 15.0, dt

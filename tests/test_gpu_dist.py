@@ -101,6 +101,10 @@ def test_bench_two_ranks_gloo_strong_scaling():
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     line = json.loads([x for x in r.stdout.decode().splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    # the N > 1 line reports rank 0's own map + local reduce (a 4-rank line once printed zeros)
+    assert line["counts"]["pairs"] > 0 and line["counts"]["sort_passes"] > 0, line["counts"]
+    assert line["roofline_sort_phase"]["frac"] > 0, line["roofline_sort_phase"]
+    assert line["roofline"]["frac"] > 0, line["roofline"]
     t, off = ii_ctypes.zipf_corpus(nb, nf, vocab, seed, threads=8)
     exp = oracle_index(t, off, list(range(nf)), threads=8)
     assert line["output_letter_sha256"] == {l: hashlib.sha256(exp[l]).hexdigest() for l in LETTERS}

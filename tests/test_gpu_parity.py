@@ -273,10 +273,13 @@ def test_narrow_key_overflow_vs_oracle():
 
 
 # ---------------------------------------------------------------- multi-GPU exchange logic
-def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False):
+def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False, pre_reduce=False):
     """G logical shards on one device: files split by the reference's size
     heuristic (ii_partition), each shard mapped in its own context, letter
-    ranges exchanged (ii_export / ii_import) and formatted by their owner."""
+    ranges exchanged (ii_export / ii_import) and formatted by their owner.
+    pre_reduce: every shard first indexes its own files alone (ii_reduce:
+    compact pairs, the token sort consumes the K1 records in place), checked
+    against the oracle, and only then exports (which must map again)."""
     import ii_dist
     n = len(off) - 1
     sizes = [off[i + 1] - off[i] for i in range(n)]
@@ -295,6 +298,9 @@ def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=Fals
             o.append(len(t))
         ix = ii_ctypes.Index(0)
         ix.map_host(bytes(t), o, fids)
+        if pre_reduce:
+            ix.reduce()
+            assert_same(ix.letters(), oracle_index(bytes(t), o, fids), "shard %d alone" % g)
         idxs.append(ix)
     los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else n, balanced=balanced)
     merged = {}
@@ -336,6 +342,15 @@ def test_logical_shards_zipf_vs_oracle():
     exp = oracle_index(text, off, list(range(300)))
     assert_same(shard_and_merge(text, off, 4), exp, "zipf G=4")
     assert_same(shard_and_merge(text, off, 4, contiguous=True), exp, "zipf G=4 contiguous")
+
+
+@pytest.mark.parametrize("case,G,balanced", [("config2", 3, False), ("zipf_small", 4, True)])
+def test_export_after_reduce(case, G, balanced):
+    # ii_reduce's compact token sort consumes the K1 records; an export plan / letter
+    # load after it must index the shard again instead of re-sorting the consumed records
+    text, off, ids, expected = case_arrays(case)
+    assert_same(shard_and_merge(text, off, G, balanced=balanced, pre_reduce=True), expected,
+                "%s G=%d export after reduce" % (case, G))
 
 
 @pytest.mark.parametrize("case,G", [("config2", 3), ("zipf_small", 8), ("edge", 4)])

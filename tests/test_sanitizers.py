@@ -128,3 +128,71 @@ def test_oracle_cli_beyond_360_files_and_list_errors(oracle_cli):
         write_list(td, names[:2], count=4)
         rc, _, err = run(oracle_cli, ["3", "7", "list.txt"], td)
         assert rc == 255 and "Error reading file name" in err
+
+
+@pytest.mark.parametrize("binary", ["plain", "san"])
+def test_cli_failed_context_exits_promptly(cli, binary):
+    """A context that fails while others are stuck (II_TEST_FAIL=map:g: context
+    g returns II_ERR_INTERNAL, every other context of the phase blocks, as
+    behind a faulted device — round 3's hang) must end the CLI at once with a
+    non-zero exit and the error on stderr, without waiting for the others."""
+    import time
+    exe = cli if binary == "san" else os.path.join(PKG, "ii_index")
+    with tempfile.TemporaryDirectory() as td:
+        write_list(td, make_files(td, 12))
+        env = dict(SAN_ENV, II_GPUS="5", II_TEST_FAIL="map:3")
+        t0 = time.time()
+        r = subprocess.run([exe, "3", "4", "list.txt"], cwd=td, capture_output=True, env=env, timeout=60)
+        dt = time.time() - t0
+        err = r.stderr.decode(errors="replace")
+    assert r.returncode == 1, err
+    assert "internal consistency check failed" in err, err
+    assert dt < 15.0, dt
+    for marker in ("AddressSanitizer", "runtime error:", "UndefinedBehaviorSanitizer"):
+        assert marker not in err, err
+
+
+@pytest.fixture(scope="module")
+def reader():
+    subprocess.run(["make", "-C", PKG, "reader_san"], check=True, stdout=subprocess.DEVNULL)
+    return os.path.join(PKG, "reader_san")
+
+
+@pytest.mark.parametrize("win,threads", [(7, 1), (64, 4), (1 << 20, 3)])
+def test_reader_windows_under_sanitizers(reader, win, threads):
+    """ii_map_files' pread reader (csrc/ii_reader.h io_fill) on
+    the host under ASan + UBSan: windows that cut files anywhere, several
+    threads, an empty file, a missing file (reported once, main.c:98, read as
+    spaces), a file shorter than its stat size (padded with spaces) and one
+    longer (the 'grown' verdict that makes ii_map_files re-read whole files)."""
+    with tempfile.TemporaryDirectory() as td:
+        specs = []  # (path, stat size given, bytes on disk or None)
+        rnd = __import__("random").Random(win)
+        for i in range(9):
+            body = bytes(rnd.choice(b"abc xyz\nQ!") for _ in range(rnd.randrange(1, 300)))
+            specs.append(("f%d.txt" % i, len(body), body))
+        specs.append(("empty.txt", 0, b""))
+        specs.append(("missing.txt", 40, None))
+        specs.append(("short.txt", 50, b"only twenty bytes ok"))
+        specs.append(("long.txt", 10, b"twenty-five bytes in here"))
+        for p, _, body in specs:
+            if body is not None:
+                with open(os.path.join(td, p), "wb") as f:
+                    f.write(body)
+        args = [str(win), str(threads)]
+        for p, size, _ in specs:
+            args += [str(size), p]
+        r = subprocess.run([reader] + args, cwd=td, capture_output=True, env=SAN_ENV, timeout=60)
+    err = r.stderr.decode(errors="replace")
+    for marker in ("AddressSanitizer", "LeakSanitizer", "runtime error:", "ThreadSanitizer"):
+        assert marker not in err, err[-3000:]
+    assert r.returncode == 0, err
+    head, _, img = r.stdout.partition(b"\n")
+    assert head == b"grown=1"
+    want = b""
+    for p, size, body in specs:
+        data = (body or b"")[:size]
+        want += data + b" " * (size - len(data)) + b"\n"
+    assert img == want
+    assert err.count("Error opening file missing.txt") == 1, err
+    assert "Mapper 1: Error opening file missing.txt" in err, err
