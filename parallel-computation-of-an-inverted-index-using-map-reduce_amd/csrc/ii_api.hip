@@ -126,7 +126,8 @@ struct ii_ctx {
     uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
     // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
     uint32_t pk_nb = 0, pk_ntb = 0;
-    int pk_F = 0, pk_L = 0;
+    int pk_F = 0, pk_L = 0, pk_m2 = 0;
+    bool pk_wide = false;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
     bool map_deep = false;   // the last map ran K1b with DeepProbe
@@ -223,6 +224,8 @@ static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 // bytes the packed token sort's u32 layout of n records may take (every bucket padded to whole tiles)
 // (n + (kRadix + 1) tiles: every bucket's last tile padded, plus the launch's whole tiles, k_onesweep_seg ncap)
 static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
+// the same padded layout of u64 records (the packed sort's MSD output for keys too wide to pack at once)
+static inline size_t wide_bytes(uint64_t n) { return sizeof(uint64_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
 // Readbacks go through the pinned words c->hbuf: a copy into pageable memory is a synchronisation of its
@@ -481,29 +484,49 @@ static int run_sort32(ii_ctx* c, uint32_t** k, uint32_t** k2, uint64_t n, int bi
     return II_OK;
 }
 
-// Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
-// W-bit key when the other W - m key bits and the F id bits fit a u32 and
-// leave two LSD passes of <= kRadixBits bits; 0 = not packable.
-static int packed_top_bits(int W, int F) {
-    if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return 0;
-    const int m = std::max(7, W + F - 32);
-    const int L = W - m;
-    return (m <= kRadixBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
+// Packed token sort (ii_prims.h, "Packed token sort"; K3 per sub-bucket,
+// ii_kernels.h k_bucket_uniq): the MSD scatter's top digit m1 of a W-bit key
+// must leave the other W - m1 key bits and the F id bits in a u32; the
+// sub-bucket pass takes the next m2 <= 8 bits and K3 the last L <= 8 (its
+// bins).  m1 is 8 bits where the u32 allows (more, smaller sub-buckets: an
+// average of ~15k records at configs[2]; II_MSD1_BITS=7 for A/B); 0 = not
+// packable (the u64 passes).
+struct PackedShape {
+    int m1 = 0, m2 = 0, L = 0;
+    bool wide = false;  // the MSD scatter writes u64 records; the sub-bucket pass packs them
+};
+static PackedShape packed_shape(int W, int F) {
+    PackedShape ps;
+    if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return ps;
+    int want = kRadixBits;
+    if (const char* e = getenv("II_MSD1_BITS")) want = std::max(1, std::min(kRadixBits, atoi(e)));
+    int m1 = std::min(want, W);
+    if (W - m1 + F > 32 && W + F - 32 <= kRadixBits) m1 = W + F - 32;  // a wider top digit packs at once
+    const int m2 = std::min(kRadixBits, W - m1);
+    const int L = W - m1 - m2;
+    if (L > kRadixBits || L + F > 32) return ps;  // (the sub-bucket records must fit a u32)
+    ps.m1 = m1;
+    ps.m2 = m2;
+    ps.L = L;
+    ps.wide = W - m1 + F > 32;
+    return ps;
 }
 
 // The token sort of local_reduce in the packed form: k_sort0_compact (dedup,
 // key remap, compaction, counts of the top digit per workgroup) into *k2, the
-// MSD scatter into buckets of u32 records (*k, padded), per-bucket digit
-// counts, two bucket-local onesweep passes (*k -> *k2 -> *k, both writing u32
-// records in the padded buckets; K3 reads that layout).  Keys sit at bits
-// [lo, lo + W) of the records, ids below 2^F.  On return *k holds the *n_out
-// sorted records.
-static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F, int m,
-                           const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
+// MSD scatter into buckets of u32 records (*k, padded to whole tiles), per
+// bucket the counts of the next m2 key bits, and one bucket-local onesweep
+// pass on those bits (*k -> *k2): sub-buckets of 2^L consecutive keys, each in
+// file order, which k_bucket_uniq (run_unique) sorts and reduces one
+// workgroup apiece.  Keys sit at bits [lo, lo + W) of the records, ids below
+// 2^F.  On return *k holds the *n_out records in sub-bucket order.
+static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F,
+                           const PackedShape& ps, const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
     *passes = 0;
     *n_out = n;
+    const int m = ps.m1;
     const uint32_t nb = 1u << m;
-    const int L = W - m, b0 = L - L / 2, b1 = L / 2;
+    const int L = W - m;  // key bits in the u32 records
     const uint64_t nch_in = c->nch_map;
     const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
     if (nch_in == 0 || group > kCMaxGroup) return II_ERR_NOMEM;
@@ -541,11 +564,15 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     HIPCK(hipGetLastError());
     CK(read_queue(c, totals + 4, 4, 4));  // (kept count, wid range: read back while the scatter runs)
     // MSD scatter: u64 records -> u32 records in padded buckets
-    const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
+    const bool ev = c->n_sc + 2 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-    k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-        *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
-        F, (1u << L) - 1u);
+    if (ps.wide)  // (u64 records in the padded buckets: the sub-bucket pass packs them)
+        k_radix_scatter<false, kScatterThreads, kScatterItems, 2><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
+            *k2, *k, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, nullptr, pad, 0, 0u);
+    else
+        k_radix_scatter<false, kScatterThreads, kScatterItems, 1><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
+            *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept,
+            reinterpret_cast<uint32_t*>(*k), pad, F, (1u << L) - 1u);
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
     uint64_t t47[4];
@@ -555,15 +582,16 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
     c->c0_bytes = 8 * n_in + 8 * n;
     *n_out = n;
-    if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
+    if (ev) c->sc_bytes[c->n_sc++] = (ps.wide ? 16 : 12) * n;
     *passes = 1;
     if (n == 0) return II_OK;
-    // per-bucket digit counts of the two LSD passes -> bases
     c->sort_packed = true;
-    c->sort_hist_bytes = 4 * n;
+    c->sort_hist_bytes = (ps.wide ? 8 : 4) * n;
     c->pk_nb = nb;
     c->pk_F = F;
     c->pk_L = L;
+    c->pk_m2 = ps.m2;
+    c->pk_wide = ps.wide;
     const uint64_t ntb = (n + kSweepTile - 1) / kSweepTile + nb;  // tiles of the padded layout, at most
     const uint32_t hg = (uint32_t)std::min<uint64_t>(kMaxChunks, ntb);
     const uint32_t per = (uint32_t)((ntb + hg - 1) / hg);
@@ -571,25 +599,36 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
-    k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
-        reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
+    // per bucket: the counts of the sub-bucket digit (the next m2 key bits; m2 = 0: one sub-bucket)
+    const int sub_shift = ps.wide ? 32 + L - ps.m2 : F + L - ps.m2;  // (wide: a bit of the u64 record)
+    if (ps.wide)
+        k_seg_hist<kSweepThreads, kSweepItems, uint64_t><<<hg, kSweepThreads, 0, c->st>>>(
+            *k, btile, bstart, nb, per, sub_shift, ps.m2, 0, 0, gh);
+    else
+        k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
+            reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, sub_shift, ps.m2, 0, 0, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
     HIPCK(hipGetLastError());
-    // two bucket-local onesweep passes, both u32 -> u32 in the padded buckets (K3 reads that layout)
-    for (int p = 0; p < 2; p++) {
+    if (ps.m2 > 0) {  // the sub-bucket pass: u32 -> u32 inside the padded buckets (k_bucket_uniq reads *k2)
         CK(lookback_pass(c, ntb * kRadix));
         const bool evp = c->n_sc < kMaxTimedPasses;
         if (evp) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        k_onesweep_seg<kSweepThreads, kSweepItems><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
-            reinterpret_cast<const uint32_t*>(p == 0 ? *k : *k2), ntb * kSweepTile,
-            reinterpret_cast<uint32_t*>(p == 0 ? *k2 : *k), btile,
-            tbk, bstart, nb, p == 0 ? F : F + b0, p == 0 ? b0 : b1, gbase + p * kRadix, 2 * kRadix, P_<uint64_t>(c->lbstat),
-            P_<uint32_t>(c->ticket), c->lb_epoch, err);
+        if (ps.wide)  // u64 in, packed u32 out: (key & (2^L - 1)) << F | id
+            k_onesweep_seg<kSweepThreads, kSweepItems, 2, true><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+                nullptr, ntb * kSweepTile, reinterpret_cast<uint32_t*>(*k2), btile, tbk, bstart, nb, sub_shift, ps.m2,
+                gbase, 2 * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err, *k,
+                (1u << (L - ps.m2)) - 1u, F);
+        else
+            k_onesweep_seg<kSweepThreads, kSweepItems><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+                reinterpret_cast<const uint32_t*>(*k), ntb * kSweepTile, reinterpret_cast<uint32_t*>(*k2), btile, tbk,
+                bstart, nb, sub_shift, ps.m2, gbase, 2 * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket),
+                c->lb_epoch, err);
         if (evp) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
-            c->sc_bytes[c->n_sc++] = 8 * n;
+            c->sc_bytes[c->n_sc++] = (ps.wide ? 12 : 8) * n;
         }
         HIPCK(hipGetLastError());
+        std::swap(*k, *k2);
         (*passes)++;
     }
     return II_OK;
@@ -638,15 +677,20 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         pe_k = P_<uint64_t>(c->pstop_w);
     }
     // one pass with decoupled look-back (k_uniq_sweep): U -> post_start[V], posting bytes -> totals[6]
-    if (packed) {  // r: the packed sort's u32 records in their padded buckets (k_uniq_sweep<true>)
+    if (packed) {  // r: the packed sort's u32 records in sub-buckets (k_bucket_uniq, one workgroup each)
         const uint64_t* bstart = P_<uint64_t>(c->msd);
         const uint32_t* btile = reinterpret_cast<const uint32_t*>(bstart + 2 * kRadix + 1);
-        const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
-        CK(lookback_pass(c, 2 * ntiles));
-        k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
-            nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
-            pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64);
+        const uint64_t* gh = bstart + 3 * kRadix + 2;
+        const uint64_t* gbase = gh + 2 * kRadix * kRadix;
+        // the sub-buckets that can hold a key: keys < NW (word ids) or < V (lexids)
+        const int Lb = c->pk_L - c->pk_m2;
+        const uint64_t nkeys = wid ? c->NW : c->V;
+        const uint64_t njobs = std::min<uint64_t>((uint64_t)c->pk_nb << c->pk_m2, ((nkeys - 1) >> Lb) + 1);
+        CK(lookback_pass(c, 2 * njobs));
+        k_bucket_uniq<<<(uint32_t)njobs, kBuNT, 0, c->st>>>(
+            reinterpret_cast<const uint32_t*>(r), btile, gh, gbase, 2 * kRadix, (uint32_t)njobs, c->pk_m2, c->pk_F,
+            c->pk_L, fmap, uniq, u32, g64, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch,
+            ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
@@ -855,7 +899,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     HIPCK(hipMemsetAsync(chunk_cnt + nch, 0, sizeof(uint64_t), c->st));  // voff[nch] = T after the scan
     c->rec_cap = use_fixed_capacity(c, nch, dense) ? kChunkCap : 0;
     if (c->rec_cap) {
-        CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, packed_bytes(nch * kChunkCap))));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, wide_bytes(nch * kChunkCap))));
         CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
         c->T = 0;
     } else {
@@ -866,7 +910,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(read_u64(c, totals + 9, &hv[1]));
         if (hv[1]) return II_ERR_LAYOUT;
         c->T = hv[0];
-        CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), wide_bytes(c->T))));
         CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
         CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
     }
@@ -1393,9 +1437,9 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     c->sort_packed = false;
     c->sort_W = lb;
     c->sort_F = F;
-    const int m = packed_top_bits(lb, F);
-    if (m)
-        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
+    const PackedShape ps = packed_shape(lb, F);
+    if (ps.m1)
+        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, ps, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
                            &sort_passes));
     else
         CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
@@ -1690,6 +1734,46 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
     return II_OK;
 }
 
+// The owner's merge of G sorted runs (back to back in *src, lengths len):
+// ceil(log2 G) rounds of pairwise merge-path merges (ii_kernels.h
+// k_merge_partition / k_merge_tiles), *src / *dst ping-pong; on return *src
+// holds the merged records.  *rounds = the rounds run.
+template <class K>
+static int merge_sources(ii_ctx* c, K** src, K** dst, std::vector<uint64_t> len, int* rounds) {
+    *rounds = 0;
+    while (len.size() > 1) {
+        MergeRound mr;
+        memset(&mr, 0, sizeof(mr));
+        mr.npairs = (uint32_t)((len.size() + 1) / 2);
+        if (mr.npairs > (uint32_t)kMergeMaxPairs) return II_ERR_ARG;
+        std::vector<uint64_t> next;
+        uint64_t a = 0, tiles = 0;
+        for (uint32_t p = 0; p < mr.npairs; p++) {
+            const uint64_t na = len[2 * p], nb = 2 * p + 1 < len.size() ? len[2 * p + 1] : 0;
+            mr.a[p] = a;
+            mr.na[p] = na;
+            mr.nb[p] = nb;
+            mr.tile0[p] = (uint32_t)tiles;
+            tiles += (na + nb + kMergeTile - 1) / kMergeTile;
+            a += na + nb;
+            next.push_back(na + nb);
+        }
+        if (tiles >= (1ull << 31)) return II_ERR_NOMEM;
+        mr.tile0[mr.npairs] = (uint32_t)tiles;
+        if (tiles) {
+            CK(grow(c->moff, sizeof(uint64_t) * (tiles + 1)));
+            uint64_t* split = P_<uint64_t>(c->moff);
+            k_merge_partition<K><<<grid_for(tiles + 1), kBlock, 0, c->st>>>(*src, mr, split);
+            k_merge_tiles<K><<<(uint32_t)tiles, kMergeNT, 0, c->st>>>(*src, *dst, mr, split);
+            HIPCK(hipGetLastError());
+        }
+        std::swap(*src, *dst);
+        len.swap(next);
+        (*rounds)++;
+    }
+    return II_OK;
+}
+
 extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64_t* recv_off, uint32_t id_bound) {
     if (!c || nparts < 1 || !recv_off || (!d_recv && nparts)) return II_ERR_ARG;
     LIVE_OR_FAIL();
@@ -1740,8 +1824,11 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     uint64_t* wrec = P_<uint64_t>(c->rec);
     uint64_t* r = P_<uint64_t>(c->rec2);
     uint64_t* r2 = P_<uint64_t>(c->rec);
-    // which merge runs (the ordered check and the measured crossover are below); the owner's sort
-    // takes u32 records lexid << F | id0 when both fit one u32
+    // how the owner orders the received pairs by (lexid, id0): sources whose id ranges ascend without
+    // overlap (ranks owning contiguous file ranges) merge as whole (word, source) runs in one scatter;
+    // interleaved ones (ii_partition's size-sorted shards) by pairwise merge-path rounds, u32 records
+    // lexid << F | id0 when both fit.  II_IMPORT_ID_SORT=1 (test knob) radix-sorts instead, =64 in the
+    // u64 form.
     bool ordered = true;
     uint64_t prev_hi1 = 0;
     for (int s = 0; s < nparts && ordered; s++) {
@@ -1750,45 +1837,35 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         if (lo1 == 0 || hi1 < lo1 || lo1 <= prev_hi1) ordered = false;
         prev_hi1 = hi1;
     }
-    constexpr int kMergeIdsMaxParts = 4;
-    const bool id_sort = getenv("II_IMPORT_ID_SORT") != nullptr;
-    const bool merge = !id_sort && (ordered || nparts <= kMergeIdsMaxParts);
+    const char* ids_env = getenv("II_IMPORT_ID_SORT");
+    const bool id_sort = ids_env != nullptr;
+    const bool scatter_runs = !id_sort && ordered;
     const int Fid = std::max(1, bitlen(id_bound ? id_bound - 1 : 0)), Lw = std::max(1, bitlen(c->V - 1));
-    const bool sort32 = !merge && Lw + Fid <= 32 && !(id_sort && !strcmp(getenv("II_IMPORT_ID_SORT"), "64"));
-    // The pairs go to r (rec2) in both forms: r2 is rec, which holds the word
-    // records wrec every source's pairs are mapped through (writing the u32
-    // records there overwrote word records later sources still read).
+    const bool use32 = !scatter_runs && Lw + Fid <= 32 && !(id_sort && !strcmp(ids_env, "64"));
+    // The pairs go to r (rec2) in every form: r2 is rec, which holds the word
+    // records wrec every source's pairs are mapped through (writing records
+    // there would overwrite word records later sources still read).
     uint64_t wbase = 0, pbase = 0;
+    std::vector<uint64_t> runs;
     for (int s = 0; s < nparts; s++) {
         const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
         const uint64_t* src = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
         const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
-        if (np && sort32)
+        if (np && use32)
             k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
                                                           reinterpret_cast<uint32_t*>(r) + pbase, Fid);
         else if (np)
             k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
         wbase += nw;
         pbase += np;
+        runs.push_back(np);
     }
     HIPCK(hipGetLastError());
-    // (lexid, id0) order.  Every source's pairs arrive sorted by (word, id0)
-    // (K3 order; local and global lexicographic ids agree in order), so the
-    // owner merges per (word, source) runs (k_merge_runs): when the sources'
-    // id ranges ascend without overlap (ranks owning contiguous file ranges)
-    // the merged order is (word, source) — k_merge_scatter moves whole runs;
-    // with interleaved ranges (ii_partition's size-sorted shards) and at most
-    // kMergeIdsMaxParts sources, k_merge_ids places every pair by binary
-    // searches of the word's other runs; with more sources (G - 1 searches per
-    // pair) the owner sorts — one LSD radix sort of u32 records lexid << F |
-    // id0 when they fit 32 bits, else LSD over the id bits, then the word bits
-    // of the u64 records.  Measured per owner (tools/exchange_timing.py, 10 GB
-    // over G interleaved shards): G = 2 merge 2.21 / u64 sort 5.25 ms, G = 4
-    // 2.16 / 3.30, G = 8 2.41 / 2.04.  II_IMPORT_ID_SORT=1 (test knob) always
-    // sorts, =64 in the u64 form.
     int p1 = 0, p2 = 0;
     c->n_sc = 0;
-    if (merge) {
+    if (scatter_runs) {
+        // Per (word, source) runs (k_merge_runs): with ascending id ranges the merged order is
+        // (word, source), so k_merge_scatter moves whole runs
         const uint64_t nk = c->V * (uint64_t)nparts;
         CK(grow(c->mstart, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
         CK(grow(c->mend, sizeof(uint64_t) * std::max<uint64_t>(nk, 1)));
@@ -1803,28 +1880,18 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
                     r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me);
             pb += np;
         }
-        uint64_t* mo = nullptr;
-        if (ordered) {
-            CK(run_scan(c, OpMergeRuns{ms, me}, nk, nullptr));
-        } else {
-            CK(grow(c->moff, sizeof(uint64_t) * (nk + 1)));
-            mo = P_<uint64_t>(c->moff);
-            CK(run_scan(c, OpRunOffsets{ms, me, mo}, nk, mo + nk));
-        }
+        CK(run_scan(c, OpMergeRuns{ms, me}, nk, nullptr));
         pb = 0;
         for (int s = 0; s < nparts; s++) {
             const uint64_t np = hdr[8 * s + 2];
-            if (np && ordered)
+            if (np)
                 k_merge_scatter<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
                     r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me, r2);
-            else if (np)
-                k_merge_ids<<<(uint32_t)std::min<uint64_t>(16384, grid_for(np)), kBlock, 0, c->st>>>(
-                    r, pb, np, (uint32_t)nparts, (uint32_t)s, ms, me, mo, r2);
             pb += np;
         }
         HIPCK(hipGetLastError());
         std::swap(r, r2);
-    } else if (sort32) {  // r holds the u32 records (its second half is the ping-pong buffer)
+    } else if (id_sort && use32) {  // (test knob) r holds the u32 records (its second half is the ping-pong buffer)
         uint32_t* a = reinterpret_cast<uint32_t*>(r);
         uint32_t* b = a + ((NP + 3) & ~3ull);  // 16-B aligned: k_radix_hist reads 16 B at a time
         CK(run_sort32(c, &a, &b, NP, Lw + Fid, &p1));
@@ -1832,9 +1899,19 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
         k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, r2);
         HIPCK(hipGetLastError());
         std::swap(r, r2);
-    } else {
+    } else if (id_sort) {  // (test knob) LSD over the id bits, then the word bits of the u64 records
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, Fid, false, &p1));
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + Lw, true, &p2));
+    } else if (use32) {  // merge-path rounds over u32 records, then the u64 records K3 reads
+        uint32_t* a = reinterpret_cast<uint32_t*>(r);
+        uint32_t* b = reinterpret_cast<uint32_t*>(r2);  // (rec: the word records are dead once mapped)
+        CK(merge_sources(c, &a, &b, runs, &p1));
+        uint64_t* out = a == reinterpret_cast<uint32_t*>(r) ? r2 : r;
+        k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, out);
+        HIPCK(hipGetLastError());
+        r = out;
+    } else {  // merge-path rounds over u64 records
+        CK(merge_sources(c, &r, &r2, runs, &p1));
     }
     HIPCK(hipEventRecord(c->ev[3], c->st));
     c->T = NP;
@@ -1971,6 +2048,12 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: bytes read + written
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
+        if (c->sort_packed) {
+            s.sort_msd_bits = (uint32_t)bitlen(c->pk_nb - 1);
+            s.sort_sub_bits = (uint32_t)c->pk_m2;
+            s.sort_bin_bits = (uint32_t)(c->pk_L - c->pk_m2);
+            s.sort_wide = c->pk_wide ? 1u : 0u;
+        }
         s.pair_bytes = c->pairs32 ? 4u : 8u;
         s.sort_key_bits = (uint32_t)c->sort_W;
         s.sort_id_bits = (uint32_t)c->sort_F;

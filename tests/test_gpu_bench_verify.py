@@ -24,7 +24,7 @@ def share_ids(p, rank, world):
     return sorted(order[sb[rank]:se[rank]])
 
 
-@pytest.mark.parametrize("name", ["config3", "config5share", "config5/share0of8"])
+@pytest.mark.parametrize("name", ["config3", "config5share", "config5/share0of8", "config5/share7of8"])
 def test_full_size_index_matches_oracle(name):
     """config5/share<r>of8: rank r's ii_partition share of configs[4] over 8
     GPUs (main.c:300-323 with M = 8), with the files' GLOBAL ids in [0, 10^6)

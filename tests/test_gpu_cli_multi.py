@@ -59,9 +59,9 @@ def test_cli_multi_gpu_partial_files(case):
 @pytest.mark.parametrize("case,G", [("config2", 3), ("zipf_small", 4), ("edge", 5)])
 @pytest.mark.parametrize("env", [{}, {"II_IMPORT_ID_SORT": "1"}, {"II_IMPORT_ID_SORT": "64"}])
 def test_cli_owner_sort_forms(case, G, env):
-    # the owners' merge of the received pairs: interleaved ids from the size heuristic take the per-pair
-    # binary-search merge (k_merge_ids) up to 4 sources and the u32 radix sort beyond (G = 5);
-    # II_IMPORT_ID_SORT=1 sorts always (u32 records), =64 sorts the u64 records — byte-identical
+    # the owners' merge of the received pairs: interleaved ids from the size heuristic take pairwise
+    # merge-path rounds (k_merge_partition / k_merge_tiles; 2 rounds at G = 3, 3 at G = 5);
+    # II_IMPORT_ID_SORT=1 radix-sorts instead (u32 records), =64 sorts the u64 records — byte-identical
     got, expected, _, _ = run_cli(case, 3, 26, dict({"II_GPUS": str(G), "II_LETTER_SPLIT": "balanced"}, **env))
     assert_same(got, expected, "%s II_GPUS=%d %s" % (case, G, env))
 

@@ -273,7 +273,7 @@ def test_narrow_key_overflow_vs_oracle():
 
 
 # ---------------------------------------------------------------- multi-GPU exchange logic
-def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False, pre_reduce=False):
+def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=False, pre_reduce=False, id_stride=1):
     """G logical shards on one device: files split by the reference's size
     heuristic (ii_partition), each shard mapped in its own context, letter
     ranges exchanged (ii_export / ii_import) and formatted by their owner.
@@ -297,12 +297,13 @@ def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=Fals
             t += text[off[f]:off[f + 1]]
             o.append(len(t))
         ix = ii_ctypes.Index(0)
-        ix.map_host(bytes(t), o, fids)
+        ix.map_host(bytes(t), o, [f * id_stride for f in fids])
         if pre_reduce:
             ix.reduce()
-            assert_same(ix.letters(), oracle_index(bytes(t), o, fids), "shard %d alone" % g)
+            assert_same(ix.letters(), oracle_index(bytes(t), o, [f * id_stride for f in fids]), "shard %d alone" % g)
         idxs.append(ix)
-    los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else n, balanced=balanced)
+    los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else (n - 1) * id_stride + 1,
+                                             balanced=balanced)
     merged = {}
     for g, ix in enumerate(idxs):
         lo, hi = los[g], his[g]
@@ -342,6 +343,12 @@ def test_logical_shards_zipf_vs_oracle():
     exp = oracle_index(text, off, list(range(300)))
     assert_same(shard_and_merge(text, off, 4), exp, "zipf G=4")
     assert_same(shard_and_merge(text, off, 4, contiguous=True), exp, "zipf G=4 contiguous")
+    # 7 owners merging 7 interleaved sources (3 merge-path rounds, the odd run carried), and ids spread
+    # to 2^27: lexid + id bits exceed 32, so the owners merge u64 records
+    assert_same(shard_and_merge(text, off, 7), exp, "zipf G=7")
+    stride = 449_000
+    exp_s = oracle_index(text, off, [f * stride for f in range(300)])
+    assert_same(shard_and_merge(text, off, 7, id_stride=stride), exp_s, "zipf G=7, ids spread to 2^27")
 
 
 @pytest.mark.parametrize("case,G,balanced", [("config2", 3, False), ("zipf_small", 4, True)])
@@ -364,8 +371,9 @@ def test_logical_shards_balanced_letters(case, G):
 def test_config5_shape_vs_oracle(nf):
     # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 / 3*10^5 files (far
     # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-3 KB
-    # files.  The packed sort runs when W + F - 32 <= 8 (W word-id bits, F file-index bits): 17-bit
-    # indices pack with the 23-bit word ids of this vocabulary, 19-bit ones take the u64 passes
+    # files.  The packed sort packs at its MSD pass when W - 8 + F <= 32 (W word-id bits, F file-index
+    # bits): 17-bit indices with the 22-bit word ids of this vocabulary; 19-bit ones (configs[4]'s last
+    # rank) are too wide: the MSD pass writes u64 records and the sub-bucket pass packs them
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
@@ -379,8 +387,11 @@ def test_config5_shape_vs_oracle(nf):
             st = ix.stats()
             assert st.deep_probe == deep
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
-    assert st.sort_packed == (st.sort_key_bits + st.sort_id_bits - 32 <= 8)
+    assert st.sort_packed == 1
+    assert st.sort_wide == (st.sort_key_bits - st.sort_msd_bits + st.sort_id_bits > 32)
     assert st.sort_id_bits == (nf - 1).bit_length()
+    if nf == 300_000:
+        assert st.sort_wide == 1
 
 
 def test_table_sized_by_last_vocabulary():
@@ -424,7 +435,8 @@ def test_large_vocab_vs_oracle_both_key_modes():
 
 def test_packed_sort_forms_vs_oracle():
     """The token sort's packed form (ii_prims.h "Packed token sort": MSD buckets
-    of u32 records, two bucket-local onesweep passes) against the u64 form
+    of u32 records, one bucket-local sub-bucket pass, k_bucket_uniq per
+    sub-bucket) against the u64 form
     (II_PACKED_SORT=0) and the oracle, for dense ids and for ids spread to 19
     and 22 bits: the records carry shard-local file indices (10 bits for 700
     files, k_chunk_files), so every shape packs and K3 maps the indices back
@@ -433,8 +445,11 @@ def test_packed_sort_forms_vs_oracle():
     off = off.tolist()
     for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 1)]:
         exp = oracle_index(t, off, ids)
-        for env in [None, "0"]:
-            if env is not None:
+        # (msd5: a 5-bit MSD digit, so the sub-buckets keep 7 key bits: 128 bins per k_bucket_uniq)
+        for env in [None, "0", "msd5"]:
+            if env == "msd5":
+                os.environ["II_MSD1_BITS"] = "5"
+            elif env is not None:
                 os.environ["II_PACKED_SORT"] = env
             try:
                 with ii_ctypes.Index(0) as ix:
@@ -442,10 +457,13 @@ def test_packed_sort_forms_vs_oracle():
                     ix.reduce()
                     assert_same(ix.letters(), exp, "ids up to %d, II_PACKED_SORT=%s" % (ids[-1], env))
                     st = ix.stats()
-                    assert st.sort_packed == (packed if env is None else 0)
+                    assert st.sort_packed == (0 if env == "0" else packed)
                     assert st.sort_bytes > 0
+                    if env == "msd5":
+                        assert st.sort_msd_bits == 5 and st.sort_bin_bits == st.sort_key_bits - 13
             finally:
                 os.environ.pop("II_PACKED_SORT", None)
+                os.environ.pop("II_MSD1_BITS", None)
 
 
 def test_global_ids_of_a_share_stay_packed():
