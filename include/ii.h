@@ -95,15 +95,11 @@ typedef struct {
     /* bytes the token sort's passes after the first move (reads + writes of
      * every scatter / onesweep launch and the packed form's bucket histogram) */
     uint64_t sort_bytes;
-    uint32_t sort_packed;  /* 1: the packed form (MSD buckets, sub-buckets of u32 records, ii_prims.h) ran */
+    uint32_t sort_packed;  /* 1: the packed form (u32 records in buckets, ii_prims.h) ran */
     uint32_t sort_key_bits;  /* W: bits of the token sort's word keys */
-    uint32_t sort_id_bits;   /* F: bits of the records' shard-local file indices (packed form: W + F - 32 <= 16) */
+    uint32_t sort_id_bits;   /* F: bits of the records' shard-local file indices (packed form: W + F - 32 <= 8) */
     uint32_t pair_bytes;     /* bytes per distinct pair K3 wrote: 4 (compact, formatted only) or 8 (exportable) */
     uint32_t deep_probe;     /* 1: the last map's K1b probed the whole bucket and the big-table home (large vocabulary) */
-    uint32_t sort_msd_bits;  /* packed form: m1 bits of the MSD buckets, m2 of the sub-buckets, L of the bins */
-    uint32_t sort_sub_bits;
-    uint32_t sort_bin_bits;
-    uint32_t sort_wide;      /* 1: the MSD pass wrote u64 records (W - m1 + F > 32), the sub-bucket pass packed them */
 } ii_stats;
 
 /* Open a context on HIP device `device`. */

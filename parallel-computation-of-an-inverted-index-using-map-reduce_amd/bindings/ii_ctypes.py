@@ -43,8 +43,6 @@ class Stats(ctypes.Structure):
         ("sort_bytes", ctypes.c_uint64), ("sort_packed", ctypes.c_uint32),
         ("sort_key_bits", ctypes.c_uint32), ("sort_id_bits", ctypes.c_uint32),
         ("pair_bytes", ctypes.c_uint32), ("deep_probe", ctypes.c_uint32),
-        ("sort_msd_bits", ctypes.c_uint32), ("sort_sub_bits", ctypes.c_uint32), ("sort_bin_bits", ctypes.c_uint32),
-        ("sort_wide", ctypes.c_uint32),
     ]
 
     def as_dict(self):

@@ -74,7 +74,7 @@ struct ii_ctx {
     DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
     DBuf uniq_x, pstart_x;  // exchange after a word-id reduce: the pairs in lexid order (letter_points)
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
-    DBuf moff;              // ii_import merge of interleaved sources: per (word, source) merged offset
+    DBuf moff;              // ii_import merge-path rounds: the left run's share before every tile (k_merge_partition)
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
     DBuf drank, g64;        // compact pairs: hot slot -> dense word index; word key of every 64th pair
     bool pairs32 = false;   // uniq holds compact u32 pairs (k_uniq_sweep uniq32): formatted, never exported
@@ -126,8 +126,7 @@ struct ii_ctx {
     uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
     // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
     uint32_t pk_nb = 0, pk_ntb = 0;
-    int pk_F = 0, pk_L = 0, pk_m2 = 0;
-    bool pk_wide = false;
+    int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
     bool map_deep = false;   // the last map ran K1b with DeepProbe
@@ -224,8 +223,6 @@ static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 // bytes the packed token sort's u32 layout of n records may take (every bucket padded to whole tiles)
 // (n + (kRadix + 1) tiles: every bucket's last tile padded, plus the launch's whole tiles, k_onesweep_seg ncap)
 static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
-// the same padded layout of u64 records (the packed sort's MSD output for keys too wide to pack at once)
-static inline size_t wide_bytes(uint64_t n) { return sizeof(uint64_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
 // Readbacks go through the pinned words c->hbuf: a copy into pageable memory is a synchronisation of its
@@ -484,49 +481,29 @@ static int run_sort32(ii_ctx* c, uint32_t** k, uint32_t** k2, uint64_t n, int bi
     return II_OK;
 }
 
-// Packed token sort (ii_prims.h, "Packed token sort"; K3 per sub-bucket,
-// ii_kernels.h k_bucket_uniq): the MSD scatter's top digit m1 of a W-bit key
-// must leave the other W - m1 key bits and the F id bits in a u32; the
-// sub-bucket pass takes the next m2 <= 8 bits and K3 the last L <= 8 (its
-// bins).  m1 is 8 bits where the u32 allows (more, smaller sub-buckets: an
-// average of ~15k records at configs[2]; II_MSD1_BITS=7 for A/B); 0 = not
-// packable (the u64 passes).
-struct PackedShape {
-    int m1 = 0, m2 = 0, L = 0;
-    bool wide = false;  // the MSD scatter writes u64 records; the sub-bucket pass packs them
-};
-static PackedShape packed_shape(int W, int F) {
-    PackedShape ps;
-    if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return ps;
-    int want = kRadixBits;
-    if (const char* e = getenv("II_MSD1_BITS")) want = std::max(1, std::min(kRadixBits, atoi(e)));
-    int m1 = std::min(want, W);
-    if (W - m1 + F > 32 && W + F - 32 <= kRadixBits) m1 = W + F - 32;  // a wider top digit packs at once
-    const int m2 = std::min(kRadixBits, W - m1);
-    const int L = W - m1 - m2;
-    if (L > kRadixBits || L + F > 32) return ps;  // (the sub-bucket records must fit a u32)
-    ps.m1 = m1;
-    ps.m2 = m2;
-    ps.L = L;
-    ps.wide = W - m1 + F > 32;
-    return ps;
+// Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
+// W-bit key when the other W - m key bits and the F id bits fit a u32 and
+// leave two LSD passes of <= kRadixBits bits; 0 = not packable.
+static int packed_top_bits(int W, int F) {
+    if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return 0;
+    const int m = std::max(7, W + F - 32);
+    const int L = W - m;
+    return (m <= kRadixBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
 }
 
 // The token sort of local_reduce in the packed form: k_sort0_compact (dedup,
 // key remap, compaction, counts of the top digit per workgroup) into *k2, the
-// MSD scatter into buckets of u32 records (*k, padded to whole tiles), per
-// bucket the counts of the next m2 key bits, and one bucket-local onesweep
-// pass on those bits (*k -> *k2): sub-buckets of 2^L consecutive keys, each in
-// file order, which k_bucket_uniq (run_unique) sorts and reduces one
-// workgroup apiece.  Keys sit at bits [lo, lo + W) of the records, ids below
-// 2^F.  On return *k holds the *n_out records in sub-bucket order.
-static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F,
-                           const PackedShape& ps, const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
+// MSD scatter into buckets of u32 records (*k, padded), per-bucket digit
+// counts, two bucket-local onesweep passes (*k -> *k2 -> *k, both writing u32
+// records in the padded buckets; K3 reads that layout).  Keys sit at bits
+// [lo, lo + W) of the records, ids below 2^F.  On return *k holds the *n_out
+// sorted records.
+static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F, int m,
+                           const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
     *passes = 0;
     *n_out = n;
-    const int m = ps.m1;
     const uint32_t nb = 1u << m;
-    const int L = W - m;  // key bits in the u32 records
+    const int L = W - m, b0 = L - L / 2, b1 = L / 2;
     const uint64_t nch_in = c->nch_map;
     const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
     if (nch_in == 0 || group > kCMaxGroup) return II_ERR_NOMEM;
@@ -564,15 +541,11 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     HIPCK(hipGetLastError());
     CK(read_queue(c, totals + 4, 4, 4));  // (kept count, wid range: read back while the scatter runs)
     // MSD scatter: u64 records -> u32 records in padded buckets
-    const bool ev = c->n_sc + 2 <= kMaxTimedPasses;
+    const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-    if (ps.wide)  // (u64 records in the padded buckets: the sub-bucket pass packs them)
-        k_radix_scatter<false, kScatterThreads, kScatterItems, 2><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-            *k2, *k, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, nullptr, pad, 0, 0u);
-    else
-        k_radix_scatter<false, kScatterThreads, kScatterItems, 1><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-            *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept,
-            reinterpret_cast<uint32_t*>(*k), pad, F, (1u << L) - 1u);
+    k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
+        *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
+        F, (1u << L) - 1u);
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
     uint64_t t47[4];
@@ -582,16 +555,15 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
     c->c0_bytes = 8 * n_in + 8 * n;
     *n_out = n;
-    if (ev) c->sc_bytes[c->n_sc++] = (ps.wide ? 16 : 12) * n;
+    if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
     *passes = 1;
     if (n == 0) return II_OK;
+    // per-bucket digit counts of the two LSD passes -> bases
     c->sort_packed = true;
-    c->sort_hist_bytes = (ps.wide ? 8 : 4) * n;
+    c->sort_hist_bytes = 4 * n;
     c->pk_nb = nb;
     c->pk_F = F;
     c->pk_L = L;
-    c->pk_m2 = ps.m2;
-    c->pk_wide = ps.wide;
     const uint64_t ntb = (n + kSweepTile - 1) / kSweepTile + nb;  // tiles of the padded layout, at most
     const uint32_t hg = (uint32_t)std::min<uint64_t>(kMaxChunks, ntb);
     const uint32_t per = (uint32_t)((ntb + hg - 1) / hg);
@@ -599,36 +571,25 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
-    // per bucket: the counts of the sub-bucket digit (the next m2 key bits; m2 = 0: one sub-bucket)
-    const int sub_shift = ps.wide ? 32 + L - ps.m2 : F + L - ps.m2;  // (wide: a bit of the u64 record)
-    if (ps.wide)
-        k_seg_hist<kSweepThreads, kSweepItems, uint64_t><<<hg, kSweepThreads, 0, c->st>>>(
-            *k, btile, bstart, nb, per, sub_shift, ps.m2, 0, 0, gh);
-    else
-        k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
-            reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, sub_shift, ps.m2, 0, 0, gh);
+    k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
+        reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
     HIPCK(hipGetLastError());
-    if (ps.m2 > 0) {  // the sub-bucket pass: u32 -> u32 inside the padded buckets (k_bucket_uniq reads *k2)
+    // two bucket-local onesweep passes, both u32 -> u32 in the padded buckets (K3 reads that layout)
+    for (int p = 0; p < 2; p++) {
         CK(lookback_pass(c, ntb * kRadix));
         const bool evp = c->n_sc < kMaxTimedPasses;
         if (evp) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        if (ps.wide)  // u64 in, packed u32 out: (key & (2^L - 1)) << F | id
-            k_onesweep_seg<kSweepThreads, kSweepItems, 2, true><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
-                nullptr, ntb * kSweepTile, reinterpret_cast<uint32_t*>(*k2), btile, tbk, bstart, nb, sub_shift, ps.m2,
-                gbase, 2 * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, err, *k,
-                (1u << (L - ps.m2)) - 1u, F);
-        else
-            k_onesweep_seg<kSweepThreads, kSweepItems><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
-                reinterpret_cast<const uint32_t*>(*k), ntb * kSweepTile, reinterpret_cast<uint32_t*>(*k2), btile, tbk,
-                bstart, nb, sub_shift, ps.m2, gbase, 2 * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket),
-                c->lb_epoch, err);
+        k_onesweep_seg<kSweepThreads, kSweepItems><<<(uint32_t)ntb, kSweepThreads, 0, c->st>>>(
+            reinterpret_cast<const uint32_t*>(p == 0 ? *k : *k2), ntb * kSweepTile,
+            reinterpret_cast<uint32_t*>(p == 0 ? *k2 : *k), btile,
+            tbk, bstart, nb, p == 0 ? F : F + b0, p == 0 ? b0 : b1, gbase + p * kRadix, 2 * kRadix, P_<uint64_t>(c->lbstat),
+            P_<uint32_t>(c->ticket), c->lb_epoch, err);
         if (evp) {
             HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
-            c->sc_bytes[c->n_sc++] = (ps.wide ? 12 : 8) * n;
+            c->sc_bytes[c->n_sc++] = 8 * n;
         }
         HIPCK(hipGetLastError());
-        std::swap(*k, *k2);
         (*passes)++;
     }
     return II_OK;
@@ -677,20 +638,15 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         pe_k = P_<uint64_t>(c->pstop_w);
     }
     // one pass with decoupled look-back (k_uniq_sweep): U -> post_start[V], posting bytes -> totals[6]
-    if (packed) {  // r: the packed sort's u32 records in sub-buckets (k_bucket_uniq, one workgroup each)
+    if (packed) {  // r: the packed sort's u32 records in their padded buckets (k_uniq_sweep<true>)
         const uint64_t* bstart = P_<uint64_t>(c->msd);
         const uint32_t* btile = reinterpret_cast<const uint32_t*>(bstart + 2 * kRadix + 1);
-        const uint64_t* gh = bstart + 3 * kRadix + 2;
-        const uint64_t* gbase = gh + 2 * kRadix * kRadix;
-        // the sub-buckets that can hold a key: keys < NW (word ids) or < V (lexids)
-        const int Lb = c->pk_L - c->pk_m2;
-        const uint64_t nkeys = wid ? c->NW : c->V;
-        const uint64_t njobs = std::min<uint64_t>((uint64_t)c->pk_nb << c->pk_m2, ((nkeys - 1) >> Lb) + 1);
-        CK(lookback_pass(c, 2 * njobs));
-        k_bucket_uniq<<<(uint32_t)njobs, kBuNT, 0, c->st>>>(
-            reinterpret_cast<const uint32_t*>(r), btile, gh, gbase, 2 * kRadix, (uint32_t)njobs, c->pk_m2, c->pk_F,
-            c->pk_L, fmap, uniq, u32, g64, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch,
-            ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW);
+        const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
+        CK(lookback_pass(c, 2 * ntiles));
+        k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
+            nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
+            pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
+            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
@@ -899,7 +855,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     HIPCK(hipMemsetAsync(chunk_cnt + nch, 0, sizeof(uint64_t), c->st));  // voff[nch] = T after the scan
     c->rec_cap = use_fixed_capacity(c, nch, dense) ? kChunkCap : 0;
     if (c->rec_cap) {
-        CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, wide_bytes(nch * kChunkCap))));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * nch * kChunkCap, packed_bytes(nch * kChunkCap))));
         CK(grow(c->pend, sizeof(uint32_t) * nch * kChunkCap));
         c->T = 0;
     } else {
@@ -910,7 +866,7 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         CK(read_u64(c, totals + 9, &hv[1]));
         if (hv[1]) return II_ERR_LAYOUT;
         c->T = hv[0];
-        CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), wide_bytes(c->T))));
+        CK(grow(c->rec, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
         CK(grow(c->rec2, std::max(sizeof(uint64_t) * std::max<uint64_t>(c->T, 1), packed_bytes(c->T))));
         CK(grow(c->pend, sizeof(uint32_t) * std::max<uint64_t>(c->T, 1)));
     }
@@ -1437,9 +1393,9 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     c->sort_packed = false;
     c->sort_W = lb;
     c->sort_F = F;
-    const PackedShape ps = packed_shape(lb, F);
-    if (ps.m1)
-        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, ps, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
+    const int m = packed_top_bits(lb, F);
+    if (m)
+        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
                            &sort_passes));
     else
         CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
@@ -2048,12 +2004,6 @@ extern "C" int ii_get_stats(ii_ctx* c, ii_stats* o) {
         s.scatter_bytes = c->n_sc ? bytes / c->n_sc : 0;  // per launch: bytes read + written
         s.sort_bytes = bytes + (c->sort_packed ? c->sort_hist_bytes : 0);
         s.sort_packed = c->sort_packed ? 1u : 0u;
-        if (c->sort_packed) {
-            s.sort_msd_bits = (uint32_t)bitlen(c->pk_nb - 1);
-            s.sort_sub_bits = (uint32_t)c->pk_m2;
-            s.sort_bin_bits = (uint32_t)(c->pk_L - c->pk_m2);
-            s.sort_wide = c->pk_wide ? 1u : 0u;
-        }
         s.pair_bytes = c->pairs32 ? 4u : 8u;
         s.sort_key_bits = (uint32_t)c->sort_W;
         s.sort_id_bits = (uint32_t)c->sort_F;

@@ -1984,355 +1984,6 @@ __global__ __launch_bounds__(kBlock) void k_wid_post(const uint32_t* __restrict_
     pe[j] = pe_w[w];
 }
 
-// ---------------------------------------------------------------- K3 per sub-bucket (packed sort)
-// The packed token sort ends with sub-buckets (ii_prims.h "Packed token
-// sort"): bucket h (the key's top m1 bits, MSD scatter) split by the next m2
-// key bits (one bucket-local onesweep pass, MSD order), so sub-bucket
-// s = h << m2 | d holds the records of 2^L consecutive word keys (L = the key
-// bits left) in the order the MSD passes kept: file order, since every pass
-// is stable and the first pass wrote the records in text order.  One
-// workgroup per sub-bucket (ticket order = key order) finishes the sort and
-// runs K3 on it at once, in place of the two LSD passes and the K3 pass over
-// the whole array (main.c:170-213: group by word, drop repeated file ids,
-// add_number; 67-77):
-//   a tile of the sub-bucket is ranked by its bin (the low L key bits:
-//   ballot match, per-wave counts, k_onesweep_seg's ranking) and reordered in
-//   LDS — stable, so a bin's records stay in file order and a repeated
-//   (word, file) record sits right after its twin (or after the bin's last
-//   record of the previous tile, kept per bin);
-//   a block scan over the reordered tile gives every kept pair its place
-//   inside its bin and its posting bytes (digits of id0 + 1, plus a space);
-//   sub-buckets of more than one tile count their bins first (phase A), then
-//   re-read and write (phase B); a single tile is ranked once.
-// The sub-bucket's pairs / posting bytes are published for the later
-// sub-buckets' look-back (K3's two granules per job); the writes are K3's:
-// uniq (u64 key << 32 | id0) or compact pairs (uniq32 + g64), P at word
-// starts and every 64th pair, post_start / post_end by word key (both known
-// here: a bin's total is counted before its first pair is written).
-constexpr int kBuNT = 512, kBuIT = 8;        // one tile = 4096 records (IT = 16: 128 VGPRs with spills)
-constexpr int kBuTile = kBuNT * kBuIT;
-constexpr int kBuMaxBins = 256;              // L <= 8 key bits per sub-bucket
-
-__global__ __launch_bounds__(kBuNT, 4) void k_bucket_uniq(
-    const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btile, const uint64_t* __restrict__ gh,
-    const uint64_t* __restrict__ gbase, uint32_t gstride, uint32_t njobs, int m2, int F, int Lp,
-    const uint32_t* __restrict__ fmap, uint64_t* __restrict__ uniq, uint32_t* __restrict__ uniq32, uint32_t* __restrict__ g64, uint64_t* __restrict__ P,
-    uint64_t* __restrict__ post_start, uint64_t* __restrict__ post_end, uint64_t* __restrict__ status,
-    uint32_t* __restrict__ ticket, uint64_t epoch, uint64_t* __restrict__ U_out, uint64_t* __restrict__ B_out,
-    unsigned long long* __restrict__ err) {
-    constexpr int NT = kBuNT, IT = kBuIT, NW = NT / 64, BW = kBuMaxBins / 64;
-    constexpr uint32_t kByteBits = 17, kByteMask = (1u << kByteBits) - 1u;  // scan value: pairs << 17 | bytes
-    static_assert((uint64_t)kBuTile * 11 <= kByteMask, "a tile's posting bytes fit the scan's byte field");
-    __shared__ uint32_t s_keys[kBuTile + 1];       // the tile, reordered by bin (+1: the position past the end)
-    __shared__ uint32_t s_wcnt[NW][kBuMaxBins];    // ranking: per-wave bin counts, then offsets
-    __shared__ uint32_t s_tstart[kBuMaxBins + 1];  // the tile's bin runs
-    __shared__ uint32_t s_e0[kBuMaxBins], s_e1[kBuMaxBins];  // scan value at a run's first position / past its last
-    __shared__ uint32_t s_lastid[kBuMaxBins];      // file index of a run's last record
-    __shared__ uint32_t s_carry[kBuMaxBins];       // file index of the bin's last record in earlier tiles (~0: none)
-    __shared__ uint32_t s_runc[kBuMaxBins];        // pairs of the bin in earlier tiles
-    __shared__ uint64_t s_runb[kBuMaxBins];        // and their posting bytes
-    __shared__ uint32_t s_bp0[kBuMaxBins + 1];     // the bins' first pair inside the sub-bucket (after phase A)
-    __shared__ uint64_t s_bb0[kBuMaxBins + 1];     // and first posting byte
-    __shared__ uint32_t s_scan[NW];
-    __shared__ uint64_t s_scan64[BW];
-    __shared__ uint64_t s_base[2];
-    __shared__ uint32_t s_tile;
-    const int t = threadIdx.x, w = wave_id(), l = lane_id();
-    if (t == 0) {  // (an earlier pass that flagged kLbTimeout left records out of place: leave, as K3)
-        const unsigned long long e0 = *err;
-        const uint32_t tk = atomicAdd(ticket, 1u);
-        s_tile = (e0 & kLbTimeout) ? ~0u : tk;
-    }
-    __syncthreads();
-    if (s_tile == ~0u) return;
-    const uint32_t job = (uint32_t)__builtin_amdgcn_readfirstlane(s_tile);
-    if (job >= njobs) return;  // (workgroup-uniform) a spare workgroup
-    const uint32_t h = job >> m2, d = job & ((1u << m2) - 1u);
-    const uint64_t n = gh[(uint64_t)h * gstride + d];
-    const uint64_t base = (uint64_t)btile[h] * kSweepTile + gbase[(uint64_t)h * gstride + d];
-    const int L = Lp - m2;
-    const uint32_t nbins = 1u << L, binmask = nbins - 1u, idmask = (1u << F) - 1u;
-    const uint64_t lt = lanemask_lt();
-    for (int i = t; i < NW * kBuMaxBins; i += NT) (&s_wcnt[0][0])[i] = 0;
-    for (int i = t; i < kBuMaxBins; i += NT) {
-        s_carry[i] = ~0u;
-        s_runc[i] = 0;
-        s_runb[i] = 0;
-    }
-    __syncthreads();
-
-    // One tile [tb, tb + tn) of the sub-bucket: ranked and reordered by bin (s_keys, s_tstart), its
-    // repeated (word, file) records found, scanned.  Every thread owns IT consecutive positions
-    // p = t * IT + j of the reordered tile (s_keys stays intact until the next tile) and keeps three
-    // words of them: fl (bit j: a kept pair), nib (4-bit posting bytes of each position: digits of
-    // id0 + 1 plus the separator, <= 11) and tbase, the block scan before its first position
-    // (kept pairs << 17 | posting bytes, tile-relative).  Per bin run: s_e0 / s_e1 = the scan at its
-    // first position and past its last, s_lastid = its last record's file index.
-    uint32_t fl = 0, tbase = 0;
-    uint64_t nib = 0;
-    auto bin_of = [&](uint32_t x) { return (x >> F) & binmask; };
-    auto load_run = [&](uint32_t* r) {
-        const uint32_t p0 = (uint32_t)t * IT;
-#pragma unroll
-        for (int q = 0; q < IT / 4; q++) {
-            const uint4 v = *reinterpret_cast<const uint4*>(&s_keys[p0 + 4 * q]);
-            r[4 * q] = v.x; r[4 * q + 1] = v.y; r[4 * q + 2] = v.z; r[4 * q + 3] = v.w;
-        }
-    };
-    auto tile_core = [&](uint64_t tb, uint32_t tn) {
-        {
-            const uint32_t wrel = (uint32_t)w * 64 * IT + (uint32_t)l;
-            uint32_t key[IT], rank[IT];
-#pragma unroll
-            for (int k = 0; k < IT; k++)
-                key[k] = wrel + (uint32_t)k * 64 < tn ? rec[base + tb + wrel + (uint64_t)k * 64] : ~0u;
-#pragma unroll
-            for (int k = 0; k < IT; k++) {  // rank inside the wave: ballot match + one LDS atomic per group
-                const bool valid = wrel + (uint32_t)k * 64 < tn;
-                const uint32_t b = bin_of(key[k]);
-                uint64_t m = __ballot(valid);
-#pragma unroll
-                for (int bit = 0; bit < 8; bit++) {
-                    if (bit < L) {
-                        const bool x = (b >> bit) & 1;
-                        const uint64_t bb = __ballot(x);
-                        m &= x ? bb : ~bb;
-                    }
-                }
-                uint32_t before = 0;
-                if (valid && (m & lt) == 0) before = atomicAdd(&s_wcnt[w][b], (uint32_t)__popcll(m));
-                const int src = valid ? (int)__builtin_ctzll(m) : l;
-                rank[k] = (uint32_t)__shfl((int)before, src, 64) + (uint32_t)__popcll(m & lt);
-            }
-            __syncthreads();
-            // bins: the tile's run starts and per-wave offsets (in place), threads t < kBuMaxBins
-            uint32_t tot = 0;
-            if ((uint32_t)t < nbins) {
-#pragma unroll
-                for (int ww = 0; ww < NW; ww++) tot += s_wcnt[ww][t];
-            }
-            const uint32_t inc = wave_incl_scan32(tot);
-            if (w < BW && l == 63) s_scan[w] = inc;
-            __syncthreads();
-            if ((uint32_t)t < nbins) {
-                uint32_t wb = 0;
-#pragma unroll
-                for (int ww = 0; ww < BW; ww++)
-                    if (ww < w) wb += s_scan[ww];
-                uint32_t run = wb + inc - tot;
-                s_tstart[t] = run;
-                if ((uint32_t)t == nbins - 1) s_tstart[nbins] = run + tot;
-#pragma unroll
-                for (int ww = 0; ww < NW; ww++) {
-                    const uint32_t c = s_wcnt[ww][t];
-                    s_wcnt[ww][t] = run;
-                    run += c;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < IT; k++)
-                if (wrel + (uint32_t)k * 64 < tn) s_keys[s_wcnt[w][bin_of(key[k])] + rank[k]] = key[k];
-            __syncthreads();
-        }
-        // (nothing reads the offsets again before the next tile's ranking, behind this tile's barriers)
-        for (int i = t; i < NW * kBuMaxBins; i += NT) (&s_wcnt[0][0])[i] = 0;
-        const uint32_t p0 = (uint32_t)t * IT;
-        uint32_t r[IT];
-        load_run(r);
-        const uint32_t before0 = t > 0 ? s_keys[p0 - 1] : ~0u;
-        const uint32_t after0 = p0 + IT < tn ? s_keys[p0 + IT] : ~0u;
-        uint32_t v = 0;
-        fl = 0;
-        nib = 0;
-        {
-            uint32_t prev = before0;
-#pragma unroll
-            for (int j = 0; j < IT; j++) {
-                const uint32_t b = bin_of(r[j]);
-                const bool first = p0 + j == 0 || bin_of(prev) != b;
-                // a repeated (word, file): the same file index as the bin's record before it (for the
-                // run's first position: the bin's last record of the earlier tiles)
-                const uint32_t pid = first ? s_carry[b] : (prev & idmask);
-                const bool keep = p0 + j < tn && (r[j] & idmask) != pid;
-                const uint32_t bytes = keep ? id_digits((uint64_t)file_id0(fmap, r[j] & idmask) + 1) + 1 : 0u;
-                v += ((uint32_t)keep << kByteBits) | bytes;
-                fl |= (uint32_t)keep << j;
-                nib |= (uint64_t)bytes << (4 * j);
-                prev = r[j];
-            }
-        }
-        const uint32_t inc = wave_incl_scan32(v);
-        if (l == 63) s_scan[w] = inc;
-        __syncthreads();
-        tbase = 0;
-#pragma unroll
-        for (int ww = 0; ww < NW; ww++)
-            if (ww < w) tbase += s_scan[ww];
-        tbase += inc - v;
-        // the runs' first / last positions record their scan values and the last file index
-        {
-            uint32_t e = tbase;
-#pragma unroll
-            for (int j = 0; j < IT; j++) {
-                const uint32_t p = p0 + (uint32_t)j;
-                const uint32_t b = bin_of(r[j]);
-                const uint32_t ej = e;
-                e += (((fl >> j) & 1u) << kByteBits) | (uint32_t)((nib >> (4 * j)) & 15u);
-                if (p >= tn) continue;
-                if (p == 0 || bin_of(j > 0 ? r[j - 1] : before0) != b) s_e0[b] = ej;
-                if (p + 1 == tn || bin_of(j + 1 < IT ? r[j + 1] : after0) != b) {
-                    s_e1[b] = e;
-                    s_lastid[b] = r[j] & idmask;
-                }
-            }
-        }
-        __syncthreads();
-    };
-    const uint32_t ntiles = (uint32_t)((n + kBuTile - 1) / kBuTile);
-    const uint64_t ep = epoch << 40;
-    const uint32_t hdkey = (h << Lp) | (d << L);  // the key bits the sub-bucket implies
-    uint64_t pbase = 0, bbase = 0;
-    // the kept pairs of the tile tile_core left (s_keys, fl, nib, tbase), at their places
-    auto write_tile = [&]() {
-        uint32_t r[IT];
-        load_run(r);
-        uint32_t e = tbase;
-#pragma unroll
-        for (int j = 0; j < IT; j++) {
-            const uint32_t ej = e;
-            e += (((fl >> j) & 1u) << kByteBits) | (uint32_t)((nib >> (4 * j)) & 15u);
-            if (!((fl >> j) & 1u)) continue;
-            const uint32_t b = bin_of(r[j]);
-            const uint32_t e0 = s_e0[b];
-            const uint32_t within = (ej >> kByteBits) - (e0 >> kByteBits);
-            const uint32_t before = s_runc[b];
-            const uint64_t u = pbase + s_bp0[b] + before + within;
-            const uint32_t key = hdkey | b;
-            const uint32_t id0 = file_id0(fmap, r[j] & idmask);
-            const bool first = before == 0 && within == 0;
-            if (uniq32) {
-                uniq32[u] = id0 | (first ? kPairFirst : 0u);
-                if ((u & 63u) == 0) g64[u >> 6] = key;
-            } else {
-                uniq[u] = ((uint64_t)key << 32) | id0;
-            }
-            if (first || (u & 63u) == 0) P[u] = bbase + s_bb0[b] + s_runb[b] + ((ej & kByteMask) - (e0 & kByteMask));
-            if (first) {
-                post_start[key] = u;
-                post_end[key] = pbase + s_bp0[b + 1];
-            }
-        }
-    };
-    // pass 0 (phase A) counts every bin's pairs and posting bytes; pass 1 (phase B) writes them — a
-    // single tile is ranked once (pass 1 writes the tile pass 0 left in s_keys and registers)
-    for (int pass = 0; pass < 2; pass++) {
-        for (uint32_t i = 0; i < ntiles; i++) {
-            if (pass == 0 || ntiles > 1) {
-                const uint64_t tb = (uint64_t)i * kBuTile;
-                tile_core(tb, (uint32_t)(n - tb < kBuTile ? n - tb : kBuTile));
-            }
-            if (pass == 1) {
-                write_tile();
-                __syncthreads();
-            }
-            if ((uint32_t)t < nbins) {  // the tile's bins into the running counts and carries
-                if (s_tstart[t + 1] != s_tstart[t]) {
-                    s_runc[t] += (s_e1[t] >> kByteBits) - (s_e0[t] >> kByteBits);
-                    s_runb[t] += (s_e1[t] & kByteMask) - (s_e0[t] & kByteMask);
-                    s_carry[t] = s_lastid[t];
-                }
-            }
-            __syncthreads();
-        }
-        if (pass == 1) break;
-        // bins -> their first pair / byte inside the sub-bucket (threads t < kBuMaxBins)
-        {
-            const uint32_t c = (uint32_t)t < nbins ? s_runc[t] : 0u;
-            const uint64_t bb = (uint32_t)t < nbins ? s_runb[t] : 0ull;
-            const uint32_t ic = wave_incl_scan32(c);
-            const uint64_t ib = wave_incl_scan(bb);
-            if (w < BW && l == 63) {
-                s_scan[w] = ic;
-                s_scan64[w] = ib;
-            }
-            __syncthreads();
-            if (t < kBuMaxBins) {
-                uint32_t wc = 0;
-                uint64_t wb = 0;
-#pragma unroll
-                for (int ww = 0; ww < BW; ww++)
-                    if (ww < w) {
-                        wc += s_scan[ww];
-                        wb += s_scan64[ww];
-                    }
-                s_bp0[t] = wc + ic - c;
-                s_bb0[t] = wb + ib - bb;
-                if (t == kBuMaxBins - 1) {
-                    s_bp0[kBuMaxBins] = wc + ic;
-                    s_bb0[kBuMaxBins] = wb + ib;
-                }
-            }
-            __syncthreads();
-        }
-        const uint64_t C = s_bp0[kBuMaxBins], B = s_bb0[kBuMaxBins];
-        // the job's aggregate at once, then the look-back over earlier jobs (K3's: wave 0, lanes 0..31
-        // walk the pair counts, 32..63 the byte counts, 32 earlier jobs per round trip)
-        if (t == 0 || t == 32)
-            __hip_atomic_store(status + 2 * (uint64_t)job + (t >> 5),
-                               ep | (job == 0 ? kLbFlagP : kLbFlagA) | (t == 0 ? C : B), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (t < 64) {
-            const uint32_t f = (uint32_t)t >> 5, jj = (uint32_t)t & 31u;
-            const uint64_t v0 = f == 0 ? C : B;
-            uint64_t excl = 0;
-            bool done = job == 0;
-            for (int64_t bse = (int64_t)job - 1; __ballot(!done) != 0; bse -= 32) {
-                uint64_t v = ep | kLbFlagP;
-                const int64_t p = bse - (int64_t)jj;
-                if (!done && p >= 0) {
-                    const uint64_t* e = status + 2 * (uint64_t)p + f;
-                    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    for (uint32_t spin = 0; (v >> 40) != epoch; spin++) {  // job p's workgroup is counting it
-                        if (spin == (1u << 24)) {
-                            atomicOr(err, kLbTimeout);
-                            v = ep | kLbFlagP;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                        v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                const uint32_t q = (uint32_t)(__ballot((v & kLbFlagP) != 0) >> (32 * f));
-                const uint32_t upto = q ? (uint32_t)__builtin_ctz(q) : 31u;
-                uint64_t add = (!done && jj <= upto) ? (v & kLbValMask) : 0;
-#pragma unroll
-                for (int o = 1; o < 32; o <<= 1) add += (uint64_t)__shfl_xor((long long)add, o, 64);
-                excl += add;
-                done = done || q != 0;
-            }
-            if (jj == 0) {
-                if (job != 0)
-                    __hip_atomic_store(status + 2 * (uint64_t)job + f, ep | kLbFlagP | (excl + v0), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                s_base[f] = excl;
-                if (job == njobs - 1) {
-                    if (f == 0) *U_out = excl + v0;
-                    else *B_out = excl + v0;
-                }
-            }
-        }
-        for (int i = t; i < kBuMaxBins; i += NT) {  // the writes count every bin again (their carry too)
-            s_carry[i] = ~0u;
-            s_runc[i] = 0;
-            s_runb[i] = 0;
-        }
-        __syncthreads();
-        pbase = s_base[0];
-        bbase = s_base[1];
-    }
-}
-
 // ---------------------------------------------------------------- K4 order
 // key = letter << dbits | (dmax - df): ascending == (letter, df desc); the
 // stable sort keeps lexicographic order among equal df (main.c:55-64).
@@ -2659,47 +2310,6 @@ __global__ __launch_bounds__(kBlock) void k_merge_runs(const uint64_t* __restric
         const uint64_t k = (uint64_t)w * G + g;
         if (i == 0 || (uint32_t)(r[pb + i - 1] >> 32) != w) rstart[k] = pb + i;
         if (i + 1 == np || (uint32_t)(r[pb + i + 1] >> 32) != w) rend[k] = pb + i + 1;
-    }
-}
-// run lengths (rend = 0: no run) -> exclusive offsets in moff (rstart / rend kept)
-struct OpRunOffsets {
-    const uint64_t* rstart;
-    const uint64_t* rend;
-    uint64_t* moff;
-    __device__ uint64_t value(uint64_t i) const { return rend[i] ? rend[i] - rstart[i] : 0; }
-    __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { moff[i] = ex; }
-};
-// Owner-side merge when the sources' id ranges interleave (ii_partition's
-// size-sorted shards, main.c:300-323): word w's pairs arrive as up to G runs,
-// one per source, each sorted by id0, and no id0 occurs in two sources (a file
-// belongs to one shard).  A pair's place in the word's merged run is its index
-// in its own run plus, for every other source, the number of that source's
-// ids below its own — a binary search of that run, whose lines the
-// neighbouring lanes share; the word's block starts at moff[w * G].  One pass
-// over the pairs of source g instead of the owner's id and word radix passes.
-__global__ __launch_bounds__(kBlock) void k_merge_ids(const uint64_t* __restrict__ r, uint64_t pb, uint64_t np,
-                                                      uint32_t G, uint32_t g, const uint64_t* __restrict__ rstart,
-                                                      const uint64_t* __restrict__ rend,
-                                                      const uint64_t* __restrict__ moff, uint64_t* __restrict__ out) {
-    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(r);  // id0 = the low dword of a pair
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t v = r[pb + i];
-        const uint32_t x = (uint32_t)v;
-        const uint64_t k0 = (uint64_t)(uint32_t)(v >> 32) * G;
-        uint64_t dst = moff[k0] + (pb + i - rstart[k0 + g]);
-        for (uint32_t s = 0; s < G; s++) {
-            const uint64_t e = s == g ? 0 : rend[k0 + s];
-            if (!e) continue;  // own run, or no run of this word in source s
-            const uint64_t b = rstart[k0 + s];
-            uint64_t lo = b, hi = e;  // first pair of the run with id0 >= x
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (r32[2 * mid] < x) lo = mid + 1;
-                else hi = mid;
-            }
-            dst += lo - b;
-        }
-        out[dst] = v;
     }
 }
 // run lengths (rend = 0: no run) -> exclusive offsets, in place in rend

@@ -242,13 +242,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const K* __restrict__ key
 // NT = 512 every digit's output run is twice as long as with 256 (the store
 // side is what bounds the pass: 6-bit passes, with twice the run length of
 // 7-bit ones, run ~15 % faster).  Threads t < kRadix own one digit each.
-// kPack (the MSD pass of the packed token sort, see k_onesweep_seg): 1 = the
+// kPack (the MSD pass of the packed token sort, see k_onesweep_seg): the
 // record (key << 32 | id) goes out as the u32 (key & pack_low) << pack_f | id
-// — the digit (the key's top bits) is implied by the bucket it lands in —, 2 =
-// it goes out whole (u64: keys too wide for a u32 until the sub-bucket pass
-// packs them); either way digit d's output starts pad[d] records later
-// (buckets padded to whole tiles).
-template <bool kHasVals, int NT = kBlock, int IT = kSortItems, int kPack = 0, class K = uint64_t>
+// — the digit (the key's top bits) is implied by the bucket it lands in — and
+// digit d's output starts pad[d] records later (buckets padded to whole tiles).
+template <bool kHasVals, int NT = kBlock, int IT = kSortItems, bool kPack = false, class K = uint64_t>
 __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin, K* __restrict__ kout,
                                                       const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
                                                       uint64_t n, uint64_t chunk, int shift, int dbits,
@@ -378,7 +376,7 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin,
                 const K k = s_keys[p];
                 const uint32_t d = (uint32_t)(k >> shift) & dmask;
                 const uint64_t dst = s_run[d] + (p - s_tstart[d]);
-                if constexpr (kPack == 1) kout32[dst] = (((uint32_t)((uint64_t)k >> 32) & pack_low) << pack_f) | (uint32_t)k;
+                if constexpr (kPack) kout32[dst] = (((uint32_t)((uint64_t)k >> 32) & pack_low) << pack_f) | (uint32_t)k;
                 else kout[dst] = k;
                 if (kHasVals) vout[dst] = s_vals[p];
             }
@@ -650,20 +648,17 @@ __global__ __launch_bounds__(kBlock) void k_tile_buckets(const uint32_t* __restr
     for (uint32_t i = btile[h] + threadIdx.x; i < btile[h + 1]; i += kBlock) tbk[i] = (uint16_t)h;
 }
 
-// Per-bucket counts of the sub-bucket digit of the packed records (and, with
-// b1 > 0, of a second digit): gh[(2 h + j) * kRadix + d] += records of bucket h
-// whose digit j is d (digit j = bits [s_j, s_j + b_j) of the record).  A
-// workgroup counts tiles [blockIdx.x * per, + per) of the padded layout with
-// 16-B loads (4 u32 / 2 u64 records a lane), and adds its counts to gh
-// whenever its tiles enter a new bucket.  K: u32 packed records, or u64 ones
-// (keys too wide to pack before the sub-bucket pass).
-template <int NT, int IT, class K = uint32_t>
-__global__ __launch_bounds__(NT) void k_seg_hist(const K* __restrict__ rec, const uint32_t* __restrict__ btile,
+// Per-bucket counts of the two LSD digits of the packed records:
+// gh[(2 h + j) * kRadix + d] += records of bucket h whose digit j is d (digit j
+// = bits [s_j, s_j + b_j) of the u32).  A workgroup counts tiles
+// [blockIdx.x * per, + per) of the padded layout, 16-B loads (4 records a lane),
+// and adds its counts to gh whenever its tiles enter a new bucket.
+template <int NT, int IT>
+__global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btile,
                                                  const uint64_t* __restrict__ bstart, uint32_t nb, uint32_t per, int s0,
                                                  int b0, int s1, int b1, uint64_t* __restrict__ gh) {
     constexpr uint32_t kTileN = NT * IT;
-    constexpr int kv = 16 / (int)sizeof(K);
-    static_assert(IT % kv == 0, "16-B loads");
+    static_assert(IT % 4 == 0, "16-B loads");
     __shared__ uint32_t c0[kRadix], c1[kRadix];
     const uint32_t t = threadIdx.x;
     const uint32_t m0 = (1u << b0) - 1u, m1 = (1u << b1) - 1u;
@@ -698,22 +693,16 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const K* __restrict__ rec, cons
         const uint64_t tb = (uint64_t)tile * kTileN;
         const uint64_t vend = (uint64_t)btile[h] * kTileN + (bstart[h + 1] - bstart[h]);
 #pragma unroll
-        for (int k = 0; k < IT / kv; k++) {
-            const uint64_t idx = tb + (uint64_t)kv * ((uint64_t)k * NT + t);
+        for (int k = 0; k < IT / 4; k++) {
+            const uint64_t idx = tb + 4ull * ((uint64_t)k * NT + t);
             if (idx >= vend) continue;
             const uint4 v = *reinterpret_cast<const uint4*>(rec + idx);
-            K r[kv];
-            if constexpr (sizeof(K) == 4) {
-                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-            } else {
-                r[0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                r[1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-            }
+            const uint32_t r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int q = 0; q < kv; q++)
+            for (int q = 0; q < 4; q++)
                 if (idx + q < vend) {
-                    atomicAdd(&c0[(uint32_t)(r[q] >> s0) & m0], 1u);
-                    if (b1) atomicAdd(&c1[(uint32_t)(r[q] >> s1) & m1], 1u);  // (b1 == 0: one digit)
+                    atomicAdd(&c0[(r[q] >> s0) & m0], 1u);
+                    atomicAdd(&c1[(r[q] >> s1) & m1], 1u);
                 }
         }
     }
@@ -727,7 +716,7 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const K* __restrict__ rec, cons
 // Digit d of bucket h starts at the bucket's padded start + dbase[h * dstride + d].
 // (launch bound of 6 waves per SIMD: without one the compiler spent 256 VGPRs
 // with spills, one workgroup per CU, 2.4x slower than k_onesweep)
-template <int NT, int IT, int kLbPer = 2, bool kWide = false>
+template <int NT, int IT, int kLbPer = 2>
 __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,
                                                      uint32_t* __restrict__ kout,
                                                      const uint32_t* __restrict__ btile,
@@ -736,15 +725,12 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
                                                      int dbits, const uint64_t* __restrict__ dbase, uint32_t dstride,
                                                      uint64_t* __restrict__ status,
                                                      uint32_t* __restrict__ ticket, uint64_t epoch,
-                                                     unsigned long long* __restrict__ err,
-                                                     const uint64_t* __restrict__ kin64 = nullptr,
-                                                     uint32_t pack_low = 0, int pack_f = 0) {
+                                                     unsigned long long* __restrict__ err) {
     constexpr int NW = NT / 64;
     constexpr int kTileN = NT * IT;
     constexpr int kDW = kRadix / 64;
     static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
     __shared__ uint32_t s_keys[kTileN];
-    __shared__ uint8_t s_dig[kWide ? kTileN : 1];  // kWide: the digit of each reordered record
     __shared__ uint32_t s_wcnt[NW][kRadix];
     __shared__ uint32_t s_tstart[kRadix];
     __shared__ uint64_t s_run[kRadix];
@@ -769,26 +755,12 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
     const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
     // the keys first (their addresses do not depend on the bucket; ncap bounds the padded layout's
     // allocation), the bucket's bounds while they are in flight
-    // kWide: u64 records (key << 32 | id, keys too wide to pack before this pass) — the digit is taken
-    // from the u64 (shift counts from bit 0 of the u64) and the record packed as the u32
-    // (key & pack_low) << pack_f | id: the bucket and the digit imply the key's other bits
     uint32_t key[IT];
-    uint32_t dg[kWide ? IT : 1];
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const uint64_t idx = wbase + (uint64_t)k * 64;
-        if constexpr (kWide) {
-            const uint64_t k64 = idx < ncap ? kin64[idx] : ~0ull;
-            dg[k] = (uint32_t)(k64 >> shift) & dmask;
-            key[k] = ((((uint32_t)(k64 >> 32)) & pack_low) << pack_f) | ((uint32_t)k64 & ((1u << pack_f) - 1u));
-        } else {
-            key[k] = idx < ncap ? kin[idx] : ~0u;
-        }
+        key[k] = idx < ncap ? kin[idx] : ~0u;
     }
-    auto digit = [&](int k) -> uint32_t {
-        if constexpr (kWide) return dg[k];
-        else return (key[k] >> shift) & dmask;
-    };
     if (tile >= btile[nb]) return;  // (workgroup-uniform) a spare workgroup of the launch's upper bound
     const uint32_t h = tbk[tile];
     const uint64_t tile0 = btile[h];
@@ -803,7 +775,7 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const bool valid = wrel + (uint32_t)k * 64 < vrel;
-        const uint32_t d = digit(k);
+        const uint32_t d = (key[k] >> shift) & dmask;
         uint64_t m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < kRadixBits; b++) {
@@ -855,11 +827,7 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-        if (wrel + (uint32_t)k * 64 < vrel) {
-            const uint32_t pos = s_wcnt[w][digit(k)] + rank[k];
-            s_keys[pos] = key[k];
-            if constexpr (kWide) s_dig[pos] = (uint8_t)dg[k];
-        }
+        if (wrel + (uint32_t)k * 64 < vrel) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
     }
     // look-back over the bucket's earlier tiles (k_onesweep's quads of lanes)
     const uint64_t obase = tile0 * kTileN;
@@ -916,8 +884,7 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
         const uint32_t p = j * NT + t;
         if (p < tile_n) {
             const uint32_t k = s_keys[p];
-            const uint32_t d = kWide ? (uint32_t)s_dig[p] : (k >> shift) & dmask;
-            kout[s_run[d] + (p - s_tstart[d])] = k;
+            kout[s_run[(k >> shift) & dmask] + (p - s_tstart[(k >> shift) & dmask])] = k;
         }
     }
 }

@@ -371,9 +371,9 @@ def test_logical_shards_balanced_letters(case, G):
 def test_config5_shape_vs_oracle(nf):
     # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 / 3*10^5 files (far
     # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-3 KB
-    # files.  The packed sort packs at its MSD pass when W - 8 + F <= 32 (W word-id bits, F file-index
-    # bits): 17-bit indices with the 22-bit word ids of this vocabulary; 19-bit ones (configs[4]'s last
-    # rank) are too wide: the MSD pass writes u64 records and the sub-bucket pass packs them
+    # files.  The packed sort runs when W + F - 32 <= 8 (W word-id bits, F file-index bits): 17-bit
+    # indices pack with the 22-bit word ids of this vocabulary, 19-bit ones (configs[4]'s last rank)
+    # take the u64 passes
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
@@ -387,11 +387,8 @@ def test_config5_shape_vs_oracle(nf):
             st = ix.stats()
             assert st.deep_probe == deep
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
-    assert st.sort_packed == 1
-    assert st.sort_wide == (st.sort_key_bits - st.sort_msd_bits + st.sort_id_bits > 32)
+    assert st.sort_packed == (st.sort_key_bits + st.sort_id_bits - 32 <= 8)
     assert st.sort_id_bits == (nf - 1).bit_length()
-    if nf == 300_000:
-        assert st.sort_wide == 1
 
 
 def test_table_sized_by_last_vocabulary():
@@ -435,8 +432,7 @@ def test_large_vocab_vs_oracle_both_key_modes():
 
 def test_packed_sort_forms_vs_oracle():
     """The token sort's packed form (ii_prims.h "Packed token sort": MSD buckets
-    of u32 records, one bucket-local sub-bucket pass, k_bucket_uniq per
-    sub-bucket) against the u64 form
+    of u32 records, two bucket-local onesweep passes) against the u64 form
     (II_PACKED_SORT=0) and the oracle, for dense ids and for ids spread to 19
     and 22 bits: the records carry shard-local file indices (10 bits for 700
     files, k_chunk_files), so every shape packs and K3 maps the indices back
@@ -445,11 +441,8 @@ def test_packed_sort_forms_vs_oracle():
     off = off.tolist()
     for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 1)]:
         exp = oracle_index(t, off, ids)
-        # (msd5: a 5-bit MSD digit, so the sub-buckets keep 7 key bits: 128 bins per k_bucket_uniq)
-        for env in [None, "0", "msd5"]:
-            if env == "msd5":
-                os.environ["II_MSD1_BITS"] = "5"
-            elif env is not None:
+        for env in [None, "0"]:
+            if env is not None:
                 os.environ["II_PACKED_SORT"] = env
             try:
                 with ii_ctypes.Index(0) as ix:
@@ -457,13 +450,10 @@ def test_packed_sort_forms_vs_oracle():
                     ix.reduce()
                     assert_same(ix.letters(), exp, "ids up to %d, II_PACKED_SORT=%s" % (ids[-1], env))
                     st = ix.stats()
-                    assert st.sort_packed == (0 if env == "0" else packed)
+                    assert st.sort_packed == (packed if env is None else 0)
                     assert st.sort_bytes > 0
-                    if env == "msd5":
-                        assert st.sort_msd_bits == 5 and st.sort_bin_bits == st.sort_key_bits - 13
             finally:
                 os.environ.pop("II_PACKED_SORT", None)
-                os.environ.pop("II_MSD1_BITS", None)
 
 
 def test_global_ids_of_a_share_stay_packed():
