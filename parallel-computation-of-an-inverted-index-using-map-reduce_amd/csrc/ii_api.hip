@@ -221,8 +221,8 @@ static inline double now_ms() {
 }
 static inline int bitlen(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 // bytes the packed token sort's u32 layout of n records may take (every bucket padded to whole tiles)
-// (n + (kRadix + 1) tiles: every bucket's last tile padded, plus the launch's whole tiles, k_onesweep_seg ncap)
-static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kRadix + 1) * kSweepTile); }
+// (n + (kMsdMax + 1) tiles: every bucket's last tile padded, plus the launch's whole tiles, k_onesweep_seg ncap)
+static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (uint64_t)(kMsdMax + 1) * kSweepTile); }
 
 // ----------------------------------------------------------------- scan / sort
 // Readbacks go through the pinned words c->hbuf: a copy into pageable memory is a synchronisation of its
@@ -320,6 +320,72 @@ static int lookback_pass(ii_ctx* c, uint64_t entries) {
     return II_OK;
 }
 
+// The first pass of a token sort (k_sort0_compact) over the K1 records *k into
+// *k2: `nranges` ranges of `group` K1b chunks, one table column each, or with
+// `half` (S0Geom) two columns per range — column h * nranges + r for half h —
+// and half 1's kept records at *k2 + n (rec2 holds 2n records then).
+struct S0Geom {
+    bool half;
+    uint64_t group, nranges, ncol;  // ncol: table columns = the scatter's workgroups
+};
+static int s0_geometry(ii_ctx* c, uint64_t n, uint64_t** k2, S0Geom* g, bool wide = false) {
+    const uint64_t nch_in = c->nch_map;
+    const char* hk = getenv("II_S0_HALF");
+    g->half = hk && !strcmp(hk, "1") && *k2 == P_<uint64_t>(c->rec2) && !wide;
+    const uint64_t maxr = g->half ? kMaxChunks / 2 : kMaxChunks;
+    g->group = (nch_in + maxr - 1) / maxr;
+    if (nch_in == 0 || g->group > kCMaxGroup) return II_ERR_NOMEM;
+    g->nranges = (nch_in + g->group - 1) / g->group;
+    g->ncol = g->half ? 2 * g->nranges : g->nranges;
+    if (g->half) {
+        CK(grow(c->rec2, std::max(sizeof(uint64_t) * 2 * std::max<uint64_t>(n, 1), packed_bytes(n))));
+        *k2 = P_<uint64_t>(c->rec2);
+    }
+    return II_OK;
+}
+// The packed sort's split first-pass output (k_sort0_compact kOut): u32
+// records at rec32[0 ..) and their top digits (u8, or u16 for wide digits) at
+// dig[0 ..), both indexed like the u64 records would be.
+struct S0Split {
+    int out = 0;  // 0: u64 records; 1: u8 digits; 2: u16 digits
+    uint32_t* rec32 = nullptr;
+    void* dig = nullptr;
+    int pack_f = 0;
+    uint32_t pack_low = 0;
+};
+template <bool kWid, bool kHalf, bool kWideD, int kOut>
+static void sort0_inst(ii_ctx* c, const S0Geom& g, uint64_t n, const uint64_t* k, uint64_t* k2, int shift,
+                       uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
+                       uint64_t* dhist, const S0Split& sp) {
+    // paired: blocks b and b + 8 of each 16 take one range's two halves (one XCD)
+    const uint32_t grid = kHalf ? (uint32_t)((g.nranges + 7) / 8 * 16) : (uint32_t)g.ncol;
+    k_sort0_compact<kWid, kHalf, kWideD, kOut><<<grid, kHalf ? kCBlock / 2 : kCBlock, 0, c->st>>>(
+        k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
+        (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files),
+        (uint32_t)g.nranges, n, sp.rec32, sp.dig, sp.pack_f, sp.pack_low);
+}
+template <bool kWid>
+static void launch_sort0_w(ii_ctx* c, const S0Geom& g, uint64_t n, const uint64_t* k, uint64_t* k2, int shift,
+                           uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1,
+                           int shift2, uint64_t* dhist, bool wide, const S0Split& sp) {
+    if (wide) {
+        if (sp.out) sort0_inst<kWid, false, true, 2>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+        else sort0_inst<kWid, false, true, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+    } else if (g.half) {
+        if (sp.out) sort0_inst<kWid, true, false, 1>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+        else sort0_inst<kWid, true, false, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+    } else {
+        if (sp.out) sort0_inst<kWid, false, false, 1>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+        else sort0_inst<kWid, false, false, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
+    }
+}
+static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, uint64_t n, const uint64_t* k, uint64_t* k2,
+                         int shift, uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept,
+                         int shift1, int shift2, uint64_t* dhist, bool wide = false, const S0Split& sp = S0Split{}) {
+    if (wid) launch_sort0_w<true>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, wide, sp);
+    else launch_sort0_w<false>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, wide, sp);
+}
+
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
 // With remap0 (token sort only, no values) the first pass is k_sort0_compact:
@@ -334,10 +400,9 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     if (n_out) *n_out = n;
     if (hi <= lo || (n <= 1 && !remap0)) return II_OK;
     if (remap0 && v) return II_ERR_INTERNAL;
-    // first pass over K1's records: one workgroup per `group` K1b chunks
-    const uint64_t nch_in = c->nch_map;
-    const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
-    if (remap0 && (nch_in == 0 || group > kCMaxGroup)) return II_ERR_NOMEM;
+    // first pass over K1's records: one workgroup (or pair) per `group` K1b chunks
+    S0Geom s0{};
+    if (remap0) CK(s0_geometry(c, n, k2, &s0));
     uint64_t nch = 0, chunk = 0;
     auto regrid = [&](uint64_t m, uint64_t tile) {
         nch = std::min<uint64_t>(kMaxChunks, (m + tile - 1) / tile);
@@ -345,7 +410,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         nch = (m + chunk - 1) / chunk;
     };
     if (remap0) {
-        nch = (nch_in + group - 1) / group;
+        nch = s0.ncol;
         chunk = 0;
     } else {
         regrid(n, kSortTile);
@@ -378,16 +443,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         uint64_t* dst = first0 ? *k : *k2;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-            if (wid)
-                k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
-                    *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist,
-                    P_<uint32_t>(c->chunk_files));
-            else
-                k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
-                    *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask,
-                    (uint32_t)nch, table, remap0, *k2, kept, lo + bits, lo + 2 * bits, dhist,
-                    P_<uint32_t>(c->chunk_files));
+            launch_sort0(c, s0, wid, n, *k, *k2, shift, dmask, table, remap0, kept, lo + bits, lo + 2 * bits, dhist);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
             if (sweep) k_digit_bases<<<kLaterDigits, kRadix, 0, c->st>>>(dhist, dhist + kLaterDigits * kRadix);
@@ -483,13 +539,36 @@ static int run_sort32(ii_ctx* c, uint32_t** k, uint32_t** k2, uint64_t n, int bi
 
 // Packed token sort (ii_prims.h, "Packed token sort"): the top digit m of a
 // W-bit key when the other W - m key bits and the F id bits fit a u32 and
-// leave two LSD passes of <= kRadixBits bits; 0 = not packable.
+// leave two LSD passes of <= kRadixBits bits; 0 = not packable.  Top digits
+// of up to kMsdMaxBits bits (k_msd_scatter_wide past kRadixBits).
+// II_PACKED_M=<m> (test knob): at least m top bits, so that small inputs reach
+// the wide split.
 static int packed_top_bits(int W, int F) {
     if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return 0;
-    const int m = std::max(7, W + F - 32);
+    const char* fm = getenv("II_PACKED_M");
+    const int m = std::max({7, W + F - 32, fm ? atoi(fm) : 0});
     const int L = W - m;
-    return (m <= kRadixBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
+    return (m <= kMsdMaxBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
 }
+
+// The packed sort's bucket geometry and LSD digit counts in c->msd (sized for
+// kMsdMax buckets): bstart[kMsdMax + 1] | pad[kMsdMax] | btile (u32)[kMsdMax + 1]
+// | gh[2 kMsdMax kRadix] | gbase[2 kMsdMax kRadix]
+struct MsdLayout {
+    uint64_t *bstart, *pad, *gh, *gbase;
+    uint32_t* btile;
+};
+static MsdLayout msd_layout(ii_ctx* c) {
+    constexpr size_t kGeo = 3 * (size_t)kMsdMax + 2;
+    MsdLayout g;
+    g.bstart = P_<uint64_t>(c->msd);
+    g.pad = g.bstart + kMsdMax + 1;
+    g.btile = reinterpret_cast<uint32_t*>(g.pad + kMsdMax);
+    g.gh = g.bstart + kGeo;
+    g.gbase = g.gh + 2 * (size_t)kMsdMax * kRadix;
+    return g;
+}
+static constexpr size_t kMsdBytes = sizeof(uint64_t) * (3 * (size_t)kMsdMax + 2 + 4 * (size_t)kMsdMax * kRadix);
 
 // The token sort of local_reduce in the packed form: k_sort0_compact (dedup,
 // key remap, compaction, counts of the top digit per workgroup) into *k2, the
@@ -504,20 +583,20 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     *n_out = n;
     const uint32_t nb = 1u << m;
     const int L = W - m, b0 = L - L / 2, b1 = L / 2;
-    const uint64_t nch_in = c->nch_map;
-    const uint64_t group = (nch_in + kMaxChunks - 1) / kMaxChunks;
-    if (nch_in == 0 || group > kCMaxGroup) return II_ERR_NOMEM;
-    const uint64_t nch = (nch_in + group - 1) / group;
-    CK(grow(c->rtable, sizeof(uint64_t) * kRadix * kMaxChunks));
+    const bool wide = m > kRadixBits;  // (k_sort0_compact<.., kWideD>, k_msd_scatter_wide)
+    const uint32_t rows = wide ? nb : kRadix;  // digit rows of the table
+    S0Geom s0{};
+    CK(s0_geometry(c, n, k2, &s0, wide));
+    const uint64_t nch = s0.ncol;
+    CK(grow(c->rtable, sizeof(uint64_t) * rows * kMaxChunks));
     CK(grow(c->kept, sizeof(uint64_t) * 2 * kMaxChunks));
-    // msd: bstart[kRadix + 1] | pad[kRadix] | btile (u32)[kRadix + 1] | gh[2 kRadix^2] | gbase[2 kRadix^2]
-    constexpr size_t kGeo = 3 * kRadix + 2;
-    CK(grow(c->msd, sizeof(uint64_t) * (kGeo + 4 * kRadix * kRadix)));
-    uint64_t* bstart = P_<uint64_t>(c->msd);
-    uint64_t* pad = bstart + kRadix + 1;
-    uint32_t* btile = reinterpret_cast<uint32_t*>(pad + kRadix);
-    uint64_t* gh = bstart + kGeo;
-    uint64_t* gbase = gh + 2 * kRadix * kRadix;
+    CK(grow(c->msd, kMsdBytes));
+    const MsdLayout g = msd_layout(c);
+    uint64_t* bstart = g.bstart;
+    uint64_t* pad = g.pad;
+    uint32_t* btile = g.btile;
+    uint64_t* gh = g.gh;
+    uint64_t* gbase = g.gbase;
     uint64_t* table = P_<uint64_t>(c->rtable);
     uint64_t* kept = P_<uint64_t>(c->kept);
     uint64_t* totals = P_<uint64_t>(c->totals);
@@ -525,17 +604,20 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const int shift = lo + L;  // the top digit of the key
     const uint32_t dmask = nb - 1u;
 
+    // the split first-pass output (II_S0_SPLIT=1): u32 records, then their digits, in *k2
+    S0Split sp;
+    const char* sk = getenv("II_S0_SPLIT");
+    if (sk && !strcmp(sk, "1")) {
+        sp.out = wide ? 2 : 1;
+        sp.rec32 = reinterpret_cast<uint32_t*>(*k2);
+        sp.dig = sp.rec32 + (s0.half ? 2 * n : n);  // (rec2 holds 8n bytes, 16n paired)
+        sp.pack_f = F;
+        sp.pack_low = (1u << L) - 1u;
+    }
     HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-    if (wid)
-        k_sort0_compact<true><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
-            *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
-            table, remap0, *k2, kept, 0, 0, nullptr, P_<uint32_t>(c->chunk_files));
-    else
-        k_sort0_compact<false><<<(uint32_t)nch, kCBlock, 0, c->st>>>(
-            *k, P_<uint64_t>(c->chunk_cnt), (uint32_t)nch_in, (uint32_t)group, c->rec_cap, shift, dmask, (uint32_t)nch,
-            table, remap0, *k2, kept, 0, 0, nullptr, P_<uint32_t>(c->chunk_files));
+    launch_sort0(c, s0, wid, n, *k, *k2, shift, dmask, table, remap0, kept, 0, 0, nullptr, wide, sp);
     HIPCK(hipEventRecord(c->ev_c0[1], c->st));
-    CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
+    CK(run_scan(c, OpInPlace{table}, (uint64_t)rows * nch, totals + 4));
     k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);
     HIPCK(hipMemsetAsync(gh, 0, sizeof(uint64_t) * 2 * nb * kRadix, c->st));
     HIPCK(hipGetLastError());
@@ -543,9 +625,27 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     // MSD scatter: u64 records -> u32 records in padded buckets
     const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-    k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
-        *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept, reinterpret_cast<uint32_t*>(*k), pad,
-        F, (1u << L) - 1u);
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(*k);
+    constexpr int NTs = kScatterThreads, ITs = kScatterItems;
+    if (sp.out == 1) {
+        k_msd_scatter<NTs, ITs, kRadix, uint8_t><<<(uint32_t)nch, NTs, 0, c->st>>>(
+            nullptr, sp.rec32, static_cast<const uint8_t*>(sp.dig), out32, shift, m, (uint32_t)nch, table, kept, pad, F,
+            sp.pack_low);
+    } else if (sp.out == 2) {
+        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512, uint16_t>
+                 : m <= 10 ? k_msd_scatter<NTs, ITs, 1024, uint16_t> : k_msd_scatter<NTs, ITs, kMsdMax, uint16_t>;
+        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(nullptr, sp.rec32, static_cast<const uint16_t*>(sp.dig), out32, shift, m,
+                                             (uint32_t)nch, table, kept, pad, F, sp.pack_low);
+    } else if (wide) {
+        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
+                                                                   : k_msd_scatter<NTs, ITs, kMsdMax>;
+        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, nullptr, nullptr, out32, shift, m, (uint32_t)nch, table, kept, pad, F,
+                                             (1u << L) - 1u);
+    } else {
+        k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
+            *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept,
+            reinterpret_cast<uint32_t*>(*k), pad, F, (1u << L) - 1u);
+    }
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
     uint64_t t47[4];
@@ -639,8 +739,9 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
     }
     // one pass with decoupled look-back (k_uniq_sweep): U -> post_start[V], posting bytes -> totals[6]
     if (packed) {  // r: the packed sort's u32 records in their padded buckets (k_uniq_sweep<true>)
-        const uint64_t* bstart = P_<uint64_t>(c->msd);
-        const uint32_t* btile = reinterpret_cast<const uint32_t*>(bstart + 2 * kRadix + 1);
+        const MsdLayout g = msd_layout(c);
+        const uint64_t* bstart = g.bstart;
+        const uint32_t* btile = g.btile;
         const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
         CK(lookback_pass(c, 2 * ntiles));
         k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(

@@ -1458,37 +1458,73 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // the onesweep passes that follow need only those global counts.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
 constexpr int kCBlock = 1024;                   // 16 waves share one 128 KiB dedup bitmap
-constexpr int kS0Items = 8;                     // records per thread per tile
+#ifndef II_S0_ITEMS  // (A/B knob, removed after the decision)
+#define II_S0_ITEMS 8
+#endif
+constexpr int kS0Items = II_S0_ITEMS;           // records per thread per tile
 constexpr int kCWaves = kCBlock / 64;
 constexpr int kCTile = kS0Items * kCBlock;      // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
 constexpr int kLaterDigits = 2;                 // digits counted for the onesweep passes
 // LDS: 16 KiB counts + 128 KiB bitmap + 4 KiB offsets + 2 KiB later digits: one workgroup per CU
 
-template <bool kWid>
-__global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
+// kHalf: TWO 512-thread workgroups per range of chunks, each with a 64 KiB
+// bitmap of half the hot level — half 0 keeps the records of hot slots [0,
+// 2^19), half 1 those of [2^19, 2^20) and of the big table — so that two
+// workgroups fit a CU (one barrier stalls while the other works).  Both read
+// the range's records (the pair are blocks b and b + 8: one XCD under the
+// observed round-robin placement, so the second read mostly hits its L2 —
+// speed only); each writes its kept records to an output region of its own
+// (half 1: past the first T records) and its digit counts to its own table
+// column (col = half * ranges + range).  Equal keys share a slot, hence a
+// half, hence a workgroup that keeps them in file order: the stable passes
+// that follow keep that order whatever the column order interleaves.
+// kWideD: top digits of up to kMsdMaxBits bits (the packed sort's wide MSD
+// split, k_msd_scatter_wide): one count row of kMsdMax digits shared by the
+// waves (16 per-wave rows would not fit beside the bitmap); rows d <= dmask.
+// kOut (the packed sort): 0 = u64 records to kout; 1 / 2 = split — the u32
+// record (key & pack_low) << pack_f | id to kout32 and its top digit (u8 / u16)
+// to kdig, at the same index (k_msd_scatter reads 5 / 6 bytes a record).
+template <bool kWid, bool kHalf = false, bool kWideD = false, int kOut = 0, int NT = kHalf ? kCBlock / 2 : kCBlock>
+__global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
                                                            const uint64_t* __restrict__ voff, uint32_t nch_in,
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
                                                            uint32_t nchunks, uint64_t* __restrict__ table,
                                                            const uint32_t* __restrict__ remap,
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
                                                            int shift1, int shift2, uint64_t* __restrict__ dhist,
-                                                           const uint32_t* __restrict__ cf) {
-    __shared__ uint32_t cnt[kCWaves][kRadix];
-    __shared__ uint32_t bm[kDedupWords];
+                                                           const uint32_t* __restrict__ cf,
+                                                           uint32_t nranges = 0, uint64_t half_off = 0,
+                                                           uint32_t* __restrict__ kout32 = nullptr,
+                                                           void* __restrict__ kdig = nullptr, int pack_f = 0,
+                                                           uint32_t pack_low = 0) {
+    constexpr int NWv = NT / 64;
+    constexpr int kTile = kS0Items * NT;
+    constexpr uint32_t kBmWords = kHalf ? kDedupWords / 2 : kDedupWords;
+    static_assert(!(kHalf && kWideD), "one or the other");
+    // (kHalf: wave pairs share a row, so two workgroups fit 160 KiB)
+    constexpr int kCntRows = kWideD ? 1 : kHalf ? NWv / 2 : NWv;
+    constexpr int kCntD = kWideD ? kMsdMax : kRadix;
+    __shared__ uint32_t cnt[kCntRows][kCntD];
+    __shared__ uint32_t bm[kBmWords];
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
     __shared__ uint32_t s_cfid[kCMaxGroup];      // narrow chunk: its file id; ~0: u64 records
     __shared__ uint32_t s_later[kLaterDigits][kRadix];
-    __shared__ uint32_t s_wtot[2][kCWaves];      // per tile parity: one barrier per tile
+    __shared__ uint32_t s_wtot[2][NWv];          // per tile parity: one barrier per tile
     __shared__ uint32_t s_last[2];               // per tile parity: file of the tile's last record
     const int w = wave_id(), l = lane_id();
-    const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
-    for (int i = threadIdx.x; i < kCWaves * kRadix; i += kCBlock) (&cnt[0][0])[i] = 0;
-    for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += kCBlock) (&s_later[0][0])[i] = 0;
-    for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
+    // kHalf: block b -> range (b / 16) * 8 + b % 8, half (b / 8) % 2; its table column half * ranges + range
+    const uint32_t range = kHalf ? (blockIdx.x / 16) * 8 + blockIdx.x % 8 : blockIdx.x;
+    const uint32_t half = kHalf ? (blockIdx.x / 8) % 2 : 0u;
+    if (kHalf && range >= nranges) return;  // (a spare block of the grid rounded to 16)
+    const uint32_t col = kHalf ? half * nranges + range : blockIdx.x;
+    const uint32_t c0 = range * group, ng = c0 + group < nch_in ? group : nch_in - c0;
+    for (int i = threadIdx.x; i < kCntRows * kCntD; i += NT) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += NT) (&s_later[0][0])[i] = 0;
+    for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = 0;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
-    for (uint32_t i = threadIdx.x; i <= ng; i += kCBlock) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
-    for (uint32_t i = threadIdx.x; i < ng; i += kCBlock) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
+    for (uint32_t i = threadIdx.x; i <= ng; i += NT) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
+    for (uint32_t i = threadIdx.x; i < ng; i += NT) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
     __syncthreads();
     const uint64_t tofs = (uint64_t)w * 64 * kS0Items + l;
     const uint64_t lt = lanemask_lt();
@@ -1499,7 +1535,8 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
     uint32_t gfid = ng ? s_cfid[0] : ~0u;            // narrow chunk's file (~0: u64 records)
-    uint64_t o = lo;  // next output position
+    uint64_t o = lo + (kHalf && half ? half_off : 0ull);  // next output position
+    const uint64_t o0 = o;
     // The next tile's records are loaded while this one is written: issued
     // after this tile's remap gathers have been consumed (vmcnt is in order, so
     // a prefetch issued before them would make the gathers wait for it).
@@ -1541,14 +1578,14 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     // the first tile's epoch: the file of the range's first record (every lane loads it)
     uint32_t epoch = lo >= hi ? 0u : s_cfid[0] != ~0u ? s_cfid[0] : (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo];
     uint32_t par = 0;
-    for (uint64_t tb = lo; tb < hi; tb += kCTile, par ^= 1u) {
+    for (uint64_t tb = lo; tb < hi; tb += kTile, par ^= 1u) {
         uint64_t raw[kS0Items];
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)
             raw[k] = nfid[k] == ~0u ? nraw[k] : ((nraw[k] >> (32 * ((nodd >> k) & 1u))) << 32) | nfid[k];
         if (tb != lo && s_last[par ^ 1u] != epoch) {  // (workgroup-uniform) a new file: clear the bitmap
             epoch = s_last[par ^ 1u];
-            for (uint32_t i = threadIdx.x; i < kDedupWords; i += kCBlock) bm[i] = 0;
+            for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = 0;
             __syncthreads();
         }
         uint32_t keep = 0, wcount = 0;
@@ -1557,9 +1594,11 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
+            if (kHalf) ok = ok && (uint32_t)(slot >= (kHotSlots >> 1)) == half;  // (big-table slots: half 1)
             if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
-                const uint32_t bit = 1u << (slot & 31);
-                ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
+                const uint32_t bs = kHalf ? (uint32_t)slot & (uint32_t)(kHotSlots / 2 - 1) : (uint32_t)slot;
+                const uint32_t bit = 1u << (bs & 31);
+                ok = !(atomicOr(&bm[bs >> 5], bit) & bit);
             }
             const uint64_t b = __ballot(ok);
             pos[k] = wcount + (uint32_t)__popcll(b & lt);
@@ -1575,26 +1614,33 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                 raw[k] = ((uint64_t)key << 32) | (raw[k] & 0xFFFFFFFFull);
             }
         if (l == 0) s_wtot[par][w] = wcount;
-        // the tile's last record (thread kCBlock - 1, item kS0Items - 1; or the range's last)
-        const uint64_t last = tb + kCTile < hi ? tb + kCTile - 1 : hi - 1;
+        // the tile's last record (thread NT - 1, item kS0Items - 1; or the range's last)
+        const uint64_t last = tb + kTile < hi ? tb + kTile - 1 : hi - 1;
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)
             if (tb + tofs + (uint64_t)k * 64 == last) s_last[par] = (uint32_t)raw[k];  // (the low half is the file)
         __syncthreads();  // (s_wtot[par] and s_last[par] are rewritten two tiles later, after the next barrier)
         uint32_t wbase = 0, ttot = 0;
 #pragma unroll
-        for (int ww = 0; ww < kCWaves; ww++) {
+        for (int ww = 0; ww < NWv; ww++) {
             const uint32_t c = s_wtot[par][ww];
             if (ww < w) wbase += c;
             ttot += c;
         }
-        if (tb + kCTile < hi) load_tile(tb + kCTile);
+        if (tb + kTile < hi) load_tile(tb + kTile);
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             if ((keep >> k) & 1u) {
                 const uint64_t r = raw[k];
-                st_nt(kout + o + wbase + pos[k], r);
-                atomicAdd(&cnt[w][(uint32_t)(r >> shift) & dmask], 1u);
+                if constexpr (kOut == 0) {
+                    st_nt(kout + o + wbase + pos[k], r);
+                } else {
+                    const uint64_t q = o + wbase + pos[k];
+                    kout32[q] = (((uint32_t)(r >> 32) & pack_low) << pack_f) | (uint32_t)r;
+                    if constexpr (kOut == 1) static_cast<uint8_t*>(kdig)[q] = (uint8_t)((r >> shift) & dmask);
+                    else static_cast<uint16_t*>(kdig)[q] = (uint16_t)((r >> shift) & dmask);
+                }
+                atomicAdd(&cnt[kWideD ? 0 : kHalf ? w >> 1 : w][(uint32_t)(r >> shift) & dmask], 1u);
                 if (dhist) {
                     atomicAdd(&s_later[0][(uint32_t)(r >> shift1) & dmask], 1u);
                     atomicAdd(&s_later[1][(uint32_t)(r >> shift2) & dmask], 1u);
@@ -1604,19 +1650,20 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         o += ttot;
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < kRadix; d += kCBlock) {
+    for (int d = threadIdx.x; d < (kWideD ? (int)dmask + 1 : kRadix); d += NT) {
         uint32_t tt = 0;
 #pragma unroll
-        for (int ww = 0; ww < kCWaves; ww++) tt += cnt[ww][d];
-        table[(uint64_t)d * nchunks + blockIdx.x] = tt;
+        for (int ww = 0; ww < kCntRows; ww++) tt += cnt[ww][d];
+        table[(uint64_t)d * nchunks + col] = tt;
+        if (kWideD) continue;  // (no later digits: the packed sort only)
         if (dhist) {
             if (s_later[0][d]) atomicAdd((unsigned long long*)&dhist[d], (unsigned long long)s_later[0][d]);
             if (s_later[1][d]) atomicAdd((unsigned long long*)&dhist[kRadix + d], (unsigned long long)s_later[1][d]);
         }
     }
     if (threadIdx.x == 0) {
-        kept[blockIdx.x] = o - lo;
-        kept[kMaxChunks + blockIdx.x] = lo;
+        kept[col] = o - o0;
+        kept[kMaxChunks + col] = o0;
     }
 }
 

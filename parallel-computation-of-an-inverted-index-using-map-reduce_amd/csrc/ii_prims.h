@@ -7,6 +7,7 @@
 // the per-chunk results, and a third kernel re-reads its chunk and writes.
 // Chunks are processed tile by tile in order, so the radix sort is stable.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -172,6 +173,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(Op op, uint64_t n, uint64
 // ----------------------------------------------------------------------------
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
+constexpr int kMsdMaxBits = 11;                    // the packed sort's top digit: up to 2048 buckets (tbk is u16)
+constexpr int kMsdMax = 1 << kMsdMaxBits;
 constexpr int kSortItems = 16;                     // keys per thread per tile
 constexpr int kSortTile = kBlock * kSortItems;     // 4096 keys per tile
 constexpr int kScatterThreads = 512;              // token-sort scatter: tiles of 512 x 16 keys (runs twice as long
@@ -383,6 +386,160 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin,
         }
         __syncthreads();
         if (digit_thread) s_run[t] += tot_d;
+        // the next iteration's first __syncthreads orders this update before use
+    }
+}
+
+// The packed token sort's MSD scatter in the u32 form: as
+// k_radix_scatter<kPack> — workgroup b reads its kept range [kept[kMaxChunks +
+// b], + kept[b]), ranks each tile by digit inside each wave (ballots, per-wave
+// counts), reorders it in LDS and writes the u32 records low << pack_f | id in
+// runs, digit d's run at its scanned table base + pad[d] — with R >= 2^m
+// digits spread over the threads (R / NT consecutive digits each; top digits
+// up to kMsdMaxBits: the F = 19 share of configs[4] needs m = 10) and the tile
+// held as the u32 records plus u16 digits, per-wave counts in u16 (a tile
+// holds < 2^16 records): 53 / 74 KiB of LDS at R = 256 / 1024.
+// D = void: the first pass left u64 records (key << 32 | id); otherwise it
+// left them split (k_sort0_compact kOut): the u32 records already packed in
+// kin32 and their top digits (D = u8 or u16) in kdig — 5 or 6 bytes a record
+// read instead of 8.
+template <int NT, int IT, int R, class D = void>
+__global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ kin32,
+                                                    const D* __restrict__ kdig, uint32_t* __restrict__ kout32,
+                                                    int shift, int dbits, uint32_t nchunks,
+                                                    const uint64_t* __restrict__ table,
+                                                    const uint64_t* __restrict__ kept,
+                                                    const uint64_t* __restrict__ pad, int pack_f, uint32_t pack_low) {
+    constexpr bool kSplit = !std::is_void<D>::value;
+    constexpr int NW = NT / 64;
+    constexpr int kTileN = NT * IT;
+    constexpr int DPT = R / NT > 0 ? R / NT : 1;  // digits per thread (threads t < R own one when R < NT)
+    static_assert((R % NT == 0 || NT % R == 0) && kTileN < 65536 && R <= kMsdMax, "u16 tile offsets");
+    __shared__ uint32_t s_keys[kTileN];
+    __shared__ uint16_t s_dig[kTileN];
+    __shared__ uint16_t s_wcnt[NW][R];
+    __shared__ uint16_t s_tstart[R];
+    __shared__ uint64_t s_run[R];
+    __shared__ uint32_t s_scan[NW];
+    const int w = wave_id(), l = lane_id(), t = threadIdx.x;
+    const uint32_t ndig = 1u << dbits, dmask = ndig - 1u;
+    const uint32_t d0 = (uint32_t)t * DPT;  // this thread's digits [d0, d0 + DPT) (those below ndig)
+    const uint64_t lo = kept[kMaxChunks + blockIdx.x], hi = lo + kept[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < DPT; i++)
+        if (d0 + i < ndig) s_run[d0 + i] = table[(uint64_t)(d0 + i) * nchunks + blockIdx.x] + pad[d0 + i];
+    const uint64_t lt = lanemask_lt();
+    uint32_t nrec[IT], ndg[IT];
+    auto load_tile = [&](uint64_t tb) {
+        const uint64_t wb = tb + (uint64_t)w * 64 * IT + l;
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const uint64_t idx = wb + (uint64_t)k * 64;
+            if constexpr (kSplit) {
+                nrec[k] = idx < hi ? kin32[idx] : 0u;
+                ndg[k] = idx < hi ? (uint32_t)kdig[idx] : 0u;
+            } else {
+                const uint64_t x = idx < hi ? kin[idx] : 0ull;
+                nrec[k] = (((uint32_t)(x >> 32) & pack_low) << pack_f) | (uint32_t)x;
+                ndg[k] = (uint32_t)(x >> shift) & dmask;
+            }
+        }
+    };
+    if (lo < hi) load_tile(lo);
+    for (uint64_t tb = lo; tb < hi; tb += kTileN) {
+#pragma unroll
+        for (int i = 0; i < DPT; i++)
+            if (d0 + i < ndig) {
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) s_wcnt[ww][d0 + i] = 0;
+            }
+        uint32_t rec[IT], dg[IT];
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            rec[k] = nrec[k];
+            dg[k] = ndg[k];
+        }
+        const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
+        __syncthreads();
+        uint32_t rank[IT];
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const bool valid = wbase + (uint64_t)k * 64 < hi;
+            const uint32_t d = dg[k];
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < kMsdMaxBits; b++) {
+                if (b < dbits) {
+                    const bool bit = (d >> b) & 1;
+                    const uint64_t bb = __ballot(bit);
+                    m &= bit ? bb : ~bb;
+                }
+            }
+            uint32_t r = 0;
+            if (valid) {
+                const uint32_t before = s_wcnt[w][d];
+                r = before + __popcll(m & lt);
+                if ((m & lt) == 0) s_wcnt[w][d] = (uint16_t)(before + __popcll(m));
+            }
+            rank[k] = r;
+        }
+        __syncthreads();
+        // this thread's digits: tile totals, then (after the block scan) the tile start and per-wave offsets
+        uint32_t tot[DPT], mine = 0;
+#pragma unroll
+        for (int i = 0; i < DPT; i++) {
+            tot[i] = 0;
+            if (d0 + i < ndig) {
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) tot[i] += s_wcnt[ww][d0 + i];
+            }
+            mine += tot[i];
+        }
+        const uint32_t inc = wave_incl_scan32(mine);
+        if (l == 63) s_scan[w] = inc;
+        __syncthreads();
+        uint32_t wb = 0, all = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) {
+            const uint32_t sv = s_scan[ww];
+            if (ww < w) wb += sv;
+            all += sv;
+        }
+        uint32_t run = wb + inc - mine;
+#pragma unroll
+        for (int i = 0; i < DPT; i++)
+            if (d0 + i < ndig) {
+                s_tstart[d0 + i] = (uint16_t)run;
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) {
+                    const uint32_t c = s_wcnt[ww][d0 + i];
+                    s_wcnt[ww][d0 + i] = (uint16_t)run;
+                    run += c;
+                }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            if (wbase + (uint64_t)k * 64 < hi) {
+                const uint32_t pos = s_wcnt[w][dg[k]] + rank[k];
+                s_keys[pos] = rec[k];
+                s_dig[pos] = (uint16_t)dg[k];
+            }
+        }
+        __syncthreads();
+        if (tb + kTileN < hi) load_tile(tb + kTileN);
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t p = j * NT + t;
+            if (p < all) {
+                const uint32_t d = s_dig[p];
+                kout32[s_run[d] + (p - s_tstart[d])] = s_keys[p];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < DPT; i++)
+            if (d0 + i < ndig) s_run[d0 + i] += tot[i];
         // the next iteration's first __syncthreads orders this update before use
     }
 }
@@ -616,28 +773,33 @@ __global__ __launch_bounds__(kRadix) void k_msd_geometry(const uint64_t* __restr
                                                          uint64_t* __restrict__ bstart, uint32_t* __restrict__ btile,
                                                          uint64_t* __restrict__ pad) {
     __shared__ uint64_t lds[kRadix / 64 + 1];
-    const uint32_t h = threadIdx.x;
     const uint64_t tot = *total;
-    const uint64_t s = h < nb ? table[(uint64_t)h * nchunks] : tot;
-    const uint64_t e = h + 1 < nb ? table[(uint64_t)(h + 1) * nchunks] : tot;
-    const uint64_t nt = h < nb ? (e - s + tile - 1) / tile : 0;
-    const uint64_t inc = wave_incl_scan(nt);
-    if (lane_id() == 63) lds[wave_id()] = inc;
-    __syncthreads();
-    uint64_t base = 0, all = 0;
-    for (int w = 0; w < kRadix / 64; w++) {
-        if (w < wave_id()) base += lds[w];
-        all += lds[w];
+    uint64_t carry = 0;  // tiles of the buckets before this round's
+    for (uint32_t hb = 0; hb < nb; hb += kRadix) {  // (nb > kRadix: the wide top digits)
+        const uint32_t h = hb + threadIdx.x;
+        const uint64_t s = h < nb ? table[(uint64_t)h * nchunks] : tot;
+        const uint64_t e = h + 1 < nb ? table[(uint64_t)(h + 1) * nchunks] : tot;
+        const uint64_t nt = h < nb ? (e - s + tile - 1) / tile : 0;
+        const uint64_t inc = wave_incl_scan(nt);
+        if (lane_id() == 63) lds[wave_id()] = inc;
+        __syncthreads();
+        uint64_t base = 0, all = 0;
+        for (int w = 0; w < kRadix / 64; w++) {
+            if (w < wave_id()) base += lds[w];
+            all += lds[w];
+        }
+        const uint64_t t0 = carry + base + inc - nt;
+        if (h < nb) {
+            bstart[h] = s;
+            btile[h] = (uint32_t)t0;
+            pad[h] = t0 * tile - s;
+        }
+        carry += all;
+        __syncthreads();  // (lds is rewritten by the next round)
     }
-    const uint64_t t0 = base + inc - nt;
-    if (h < nb) {
-        bstart[h] = s;
-        btile[h] = (uint32_t)t0;
-        pad[h] = t0 * tile - s;
-    }
-    if (h == 0) {
+    if (threadIdx.x == 0) {
         bstart[nb] = tot;
-        btile[nb] = (uint32_t)all;
+        btile[nb] = (uint32_t)carry;
     }
 }
 

@@ -371,9 +371,9 @@ def test_logical_shards_balanced_letters(case, G):
 def test_config5_shape_vs_oracle(nf):
     # BASELINE configs[4]'s shape at a size the oracle finishes in seconds: 10^5 / 3*10^5 files (far
     # beyond the reference's 360, main.c:8), vocabulary 10^7 (most words overflow the hot level), 1-3 KB
-    # files.  The packed sort runs when W + F - 32 <= 8 (W word-id bits, F file-index bits): 17-bit
-    # indices pack with the 22-bit word ids of this vocabulary, 19-bit ones (configs[4]'s last rank)
-    # take the u64 passes
+    # files.  The packed sort runs when W + F - 32 <= 11 (W word-id bits, F file-index bits): 17-bit
+    # indices pack with the 22-bit word ids of this vocabulary under an 8-bit top digit, 19-bit ones
+    # (configs[4]'s last rank) under a 9-bit one (k_msd_scatter_wide)
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
@@ -387,7 +387,7 @@ def test_config5_shape_vs_oracle(nf):
             st = ix.stats()
             assert st.deep_probe == deep
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
-    assert st.sort_packed == (st.sort_key_bits + st.sort_id_bits - 32 <= 8)
+    assert st.sort_packed == 1 and st.sort_key_bits + st.sort_id_bits - 32 <= 11
     assert st.sort_id_bits == (nf - 1).bit_length()
 
 
@@ -454,6 +454,37 @@ def test_packed_sort_forms_vs_oracle():
                     assert st.sort_bytes > 0
             finally:
                 os.environ.pop("II_PACKED_SORT", None)
+
+
+@pytest.mark.parametrize("env", [{"II_PACKED_M": "9"}, {"II_PACKED_M": "10"}, {"II_PACKED_M": "11"},
+                                 {"II_S0_HALF": "1"}, {"II_S0_HALF": "1", "II_PACKED_SORT": "0"},
+                                 {"II_S0_HALF": "1", "II_SORT_KEYS": "lexid"}, {"II_S0_SPLIT": "1"},
+                                 {"II_S0_SPLIT": "1", "II_PACKED_M": "10"}, {"II_S0_SPLIT": "1", "II_S0_HALF": "1"}])
+def test_sort_first_pass_forms_vs_oracle(env):
+    """The token sort's wide top digit (II_PACKED_M forces m top bits: the
+    wide MSD split k_msd_scatter_wide and k_sort0_compact's wide count row, the
+    form configs[4]'s F = 19 share takes) and the paired first pass (II_S0_HALF:
+    two half-bitmap workgroups per range, k_sort0_compact<.., kHalf>) and its
+    split output (II_S0_SPLIT: u32 records + top digits, k_msd_scatter) in the
+    packed and u64 sorts and with both key kinds, against the oracle; ids
+    spread to 22 bits and 700 files of very different sizes."""
+    t, off = ii_ctypes.zipf_corpus(48_000_000, 700, 3_000_000, 29, threads=8)
+    off = off.tolist()
+    ids = [6007 * i for i in range(700)]
+    exp = oracle_index(t, off, ids)
+    try:
+        os.environ.update(env)
+        with ii_ctypes.Index(0) as ix:
+            for rep in range(2):  # (the second map reuses the grown buffers)
+                ix.map_host(t, off, ids)
+                ix.reduce()
+                assert_same(ix.letters(), exp, "%s rep %d" % (env, rep))
+            st = ix.stats()
+            assert st.sort_packed == (0 if env.get("II_PACKED_SORT") == "0" else 1)
+            assert st.sort_bytes > 0
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
 
 
 def test_global_ids_of_a_share_stay_packed():
