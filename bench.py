@@ -639,7 +639,8 @@ def main():
         # sort + segmented-reduce phase (K2 token sort + K3 unique), three byte counts:
         #  impl (frac, the primary figure): the bytes this build's kernels must move —
         #          the first pass reads T records (u32 / u64 as K1 wrote them, counted
-        #          as 8 B) and writes the T_k kept ones, the passes after it as the
+        #          as 8 B) and writes the T_k kept ones (st.sort0_bytes: 8 B each, or
+        #          the split form's u32 + digit), the passes after it as the
         #          library counts them (st.sort_bytes: the packed form's u32 bucket
         #          passes), K3 reads the sorted records once (u32 in the packed form)
         #          and writes the pairs, the posting offsets P (every word start and
@@ -656,7 +657,7 @@ def main():
         k3_read = (4 if st.sort_packed else 8) * Tk  # the packed form's K3 reads u32 records
         # (the pairs: 4 B each when K3 wrote the compact form, plus the word key of every 64th)
         pair_b = (4 * U + 4 * (U // 64)) if st.pair_bytes == 4 else 8 * U
-        impl_b = 8 * T + 8 * Tk + st.sort_bytes + k3_read + pair_b + 8 * (V + U // 64) + 16 * V
+        impl_b = st.sort0_bytes + st.sort_bytes + k3_read + pair_b + 8 * (V + U // 64) + 16 * V
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_gbs = impl_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         pmc_b = pmc_phase_bytes(traffic) if traffic else None

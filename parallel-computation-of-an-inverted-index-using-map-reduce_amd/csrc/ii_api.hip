@@ -126,6 +126,7 @@ struct ii_ctx {
     uint64_t sort_hist_bytes = 0;  // its bucket-histogram reads
     // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
     uint32_t pk_nb = 0, pk_ntb = 0;
+    uint64_t pk_ncap = 0;  // u32 records K3 may load (the padded layout's extent)
     int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
@@ -653,9 +654,10 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const uint64_t n_in = n;
     n = t47[0];
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
-    c->c0_bytes = 8 * n_in + 8 * n;
+    const uint64_t kept_b = sp.out ? 4 + sp.out : 8;  // bytes of a kept record between the first pass and the MSD
+    c->c0_bytes = 8 * n_in + kept_b * n;
     *n_out = n;
-    if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
+    if (ev) c->sc_bytes[c->n_sc++] = (kept_b + 4) * n;
     *passes = 1;
     if (n == 0) return II_OK;
     // per-bucket digit counts of the two LSD passes -> bases
@@ -668,6 +670,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const uint32_t hg = (uint32_t)std::min<uint64_t>(kMaxChunks, ntb);
     const uint32_t per = (uint32_t)((ntb + hg - 1) / hg);
     c->pk_ntb = (uint32_t)ntb;
+    c->pk_ncap = ntb * kSweepTile;
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
@@ -745,7 +748,7 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
         CK(lookback_pass(c, 2 * ntiles));
         k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
-            nullptr, n, reinterpret_cast<const uint32_t*>(r), (uint64_t)c->pk_ntb * kSweepTile, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
+            nullptr, n, reinterpret_cast<const uint32_t*>(r), c->pk_ncap, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
             P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64);
     } else {
@@ -1959,14 +1962,29 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     } else if (id_sort) {  // (test knob) LSD over the id bits, then the word bits of the u64 records
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 0, Fid, false, &p1));
         CK(run_sort(c, &r, &r2, nullptr, nullptr, NP, 32, 32 + Lw, true, &p2));
-    } else if (use32) {  // merge-path rounds over u32 records, then the u64 records K3 reads
+    } else if (use32) {  // merge-path rounds over u32 records; K3 reads them as one bucket of the packed form
         uint32_t* a = reinterpret_cast<uint32_t*>(r);
         uint32_t* b = reinterpret_cast<uint32_t*>(r2);  // (rec: the word records are dead once mapped)
         CK(merge_sources(c, &a, &b, runs, &p1));
-        uint64_t* out = a == reinterpret_cast<uint32_t*>(r) ? r2 : r;
-        k_unpack32<<<(uint32_t)std::min<uint64_t>(16384, grid_for(NP)), kBlock, 0, c->st>>>(a, NP, Fid, out);
+        const uint64_t ntb = (NP + kSweepTile - 1) / kSweepTile;
+        CK(grow(c->msd, kMsdBytes));
+        CK(grow(c->tbk, sizeof(uint16_t) * ntb));
+        const MsdLayout g = msd_layout(c);
+        HIPCK(hipMemsetAsync(c->tbk.p, 0, sizeof(uint16_t) * ntb, c->st));
+        k_one_bucket<<<1, 1, 0, c->st>>>(g.bstart, g.btile, NP, (uint32_t)ntb);
         HIPCK(hipGetLastError());
-        r = out;
+        c->pk_nb = 1;
+        c->pk_ntb = (uint32_t)ntb;
+        c->pk_ncap = NP;
+        c->pk_F = Fid;
+        c->pk_L = Lw;
+        HIPCK(hipEventRecord(c->ev[3], c->st));
+        c->T = NP;
+        CK(run_unique(c, reinterpret_cast<const uint64_t*>(a), NP, false, true, nullptr, true));
+        HIPCK(hipEventRecord(c->ev[4], c->st));
+        c->stats.sort_passes = (uint32_t)p1;
+        c->have_pairs = true;
+        return II_OK;
     } else {  // merge-path rounds over u64 records
         CK(merge_sources(c, &r, &r2, runs, &p1));
     }

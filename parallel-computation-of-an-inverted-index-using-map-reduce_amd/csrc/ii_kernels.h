@@ -1458,10 +1458,7 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // the onesweep passes that follow need only those global counts.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
 constexpr int kCBlock = 1024;                   // 16 waves share one 128 KiB dedup bitmap
-#ifndef II_S0_ITEMS  // (A/B knob, removed after the decision)
-#define II_S0_ITEMS 8
-#endif
-constexpr int kS0Items = II_S0_ITEMS;           // records per thread per tile
+constexpr int kS0Items = 8;                     // records per thread per tile (12, 16: spills)
 constexpr int kCWaves = kCBlock / 64;
 constexpr int kCTile = kS0Items * kCBlock;      // records per tile
 constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS offsets)
@@ -2332,6 +2329,15 @@ __global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restr
         if (k32) static_cast<uint32_t*>(out)[i] = (remap[slot] << f32) | (uint32_t)r;
         else static_cast<uint64_t*>(out)[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
     }
+}
+// The packed layout's geometry for ONE bucket of n u32 records from index 0
+// (the owner's merged u32 pairs, read by k_uniq_sweep<true> as bucket 0:
+// lexid = record >> F, as the packed sort's bucket-0 words)
+__global__ void k_one_bucket(uint64_t* __restrict__ bstart, uint32_t* __restrict__ btile, uint64_t n, uint32_t ntb) {
+    bstart[0] = 0;
+    bstart[1] = n;
+    btile[0] = 0;
+    btile[1] = ntb;
 }
 // u32 records lexid << f | id0 -> the u64 records lexid << 32 | id0 K3 reads
 __global__ __launch_bounds__(kBlock) void k_unpack32(const uint32_t* __restrict__ in, uint64_t n, int f,
