@@ -639,8 +639,7 @@ def main():
         # sort + segmented-reduce phase (K2 token sort + K3 unique), three byte counts:
         #  impl (frac, the primary figure): the bytes this build's kernels must move —
         #          the first pass reads T records (u32 / u64 as K1 wrote them, counted
-        #          as 8 B) and writes the T_k kept ones (st.sort0_bytes: 8 B each, or
-        #          the split form's u32 + digit), the passes after it as the
+        #          as 8 B) and writes the T_k kept ones (st.sort0_bytes), the passes after it as the
         #          library counts them (st.sort_bytes: the packed form's u32 bucket
         #          passes), K3 reads the sorted records once (u32 in the packed form)
         #          and writes the pairs, the posting offsets P (every word start and

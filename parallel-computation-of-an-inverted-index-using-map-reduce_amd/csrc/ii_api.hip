@@ -127,6 +127,7 @@ struct ii_ctx {
     // packed form: the sorted u32 records' layout (bucket geometry in msd, bits), for K3
     uint32_t pk_nb = 0, pk_ntb = 0;
     uint64_t pk_ncap = 0;  // u32 records K3 may load (the padded layout's extent)
+    int ncu = 256;         // compute units (persistent launches)
     int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
@@ -322,69 +323,32 @@ static int lookback_pass(ii_ctx* c, uint64_t entries) {
 }
 
 // The first pass of a token sort (k_sort0_compact) over the K1 records *k into
-// *k2: `nranges` ranges of `group` K1b chunks, one table column each, or with
-// `half` (S0Geom) two columns per range — column h * nranges + r for half h —
-// and half 1's kept records at *k2 + n (rec2 holds 2n records then).
+// *k2: one workgroup per `group` K1b chunks (at most kMaxChunks workgroups),
+// one table column each.
 struct S0Geom {
-    bool half;
-    uint64_t group, nranges, ncol;  // ncol: table columns = the scatter's workgroups
+    uint64_t group, ncol;  // ncol: workgroups = table columns = the scatter's workgroups
 };
-static int s0_geometry(ii_ctx* c, uint64_t n, uint64_t** k2, S0Geom* g, bool wide = false) {
+static int s0_geometry(ii_ctx* c, S0Geom* g) {
     const uint64_t nch_in = c->nch_map;
-    const char* hk = getenv("II_S0_HALF");
-    g->half = hk && !strcmp(hk, "1") && *k2 == P_<uint64_t>(c->rec2) && !wide;
-    const uint64_t maxr = g->half ? kMaxChunks / 2 : kMaxChunks;
-    g->group = (nch_in + maxr - 1) / maxr;
+    g->group = (nch_in + kMaxChunks - 1) / kMaxChunks;
     if (nch_in == 0 || g->group > kCMaxGroup) return II_ERR_NOMEM;
-    g->nranges = (nch_in + g->group - 1) / g->group;
-    g->ncol = g->half ? 2 * g->nranges : g->nranges;
-    if (g->half) {
-        CK(grow(c->rec2, std::max(sizeof(uint64_t) * 2 * std::max<uint64_t>(n, 1), packed_bytes(n))));
-        *k2 = P_<uint64_t>(c->rec2);
-    }
+    g->ncol = (nch_in + g->group - 1) / g->group;
     return II_OK;
 }
-// The packed sort's split first-pass output (k_sort0_compact kOut): u32
-// records at rec32[0 ..) and their top digits (u8, or u16 for wide digits) at
-// dig[0 ..), both indexed like the u64 records would be.
-struct S0Split {
-    int out = 0;  // 0: u64 records; 1: u8 digits; 2: u16 digits
-    uint32_t* rec32 = nullptr;
-    void* dig = nullptr;
-    int pack_f = 0;
-    uint32_t pack_low = 0;
-};
-template <bool kWid, bool kHalf, bool kWideD, int kOut>
-static void sort0_inst(ii_ctx* c, const S0Geom& g, uint64_t n, const uint64_t* k, uint64_t* k2, int shift,
-                       uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
-                       uint64_t* dhist, const S0Split& sp) {
-    // paired: blocks b and b + 8 of each 16 take one range's two halves (one XCD)
-    const uint32_t grid = kHalf ? (uint32_t)((g.nranges + 7) / 8 * 16) : (uint32_t)g.ncol;
-    k_sort0_compact<kWid, kHalf, kWideD, kOut><<<grid, kHalf ? kCBlock / 2 : kCBlock, 0, c->st>>>(
+template <bool kWid, bool kWideD>
+static void sort0_inst(ii_ctx* c, const S0Geom& g, const uint64_t* k, uint64_t* k2, int shift, uint32_t dmask,
+                       uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2, uint64_t* dhist) {
+    k_sort0_compact<kWid, kWideD><<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
         k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
-        (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files),
-        (uint32_t)g.nranges, n, sp.rec32, sp.dig, sp.pack_f, sp.pack_low);
+        (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files));
 }
-template <bool kWid>
-static void launch_sort0_w(ii_ctx* c, const S0Geom& g, uint64_t n, const uint64_t* k, uint64_t* k2, int shift,
-                           uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1,
-                           int shift2, uint64_t* dhist, bool wide, const S0Split& sp) {
-    if (wide) {
-        if (sp.out) sort0_inst<kWid, false, true, 2>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-        else sort0_inst<kWid, false, true, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-    } else if (g.half) {
-        if (sp.out) sort0_inst<kWid, true, false, 1>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-        else sort0_inst<kWid, true, false, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-    } else {
-        if (sp.out) sort0_inst<kWid, false, false, 1>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-        else sort0_inst<kWid, false, false, 0>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, sp);
-    }
-}
-static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, uint64_t n, const uint64_t* k, uint64_t* k2,
-                         int shift, uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept,
-                         int shift1, int shift2, uint64_t* dhist, bool wide = false, const S0Split& sp = S0Split{}) {
-    if (wid) launch_sort0_w<true>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, wide, sp);
-    else launch_sort0_w<false>(c, g, n, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist, wide, sp);
+static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k, uint64_t* k2, int shift,
+                         uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
+                         uint64_t* dhist, bool wide = false) {
+    if (wid && wide) sort0_inst<true, true>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
+    else if (wid) sort0_inst<true, false>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
+    else if (wide) sort0_inst<false, true>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
+    else sort0_inst<false, false>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
 }
 
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
@@ -403,7 +367,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     if (remap0 && v) return II_ERR_INTERNAL;
     // first pass over K1's records: one workgroup (or pair) per `group` K1b chunks
     S0Geom s0{};
-    if (remap0) CK(s0_geometry(c, n, k2, &s0));
+    if (remap0) CK(s0_geometry(c, &s0));
     uint64_t nch = 0, chunk = 0;
     auto regrid = [&](uint64_t m, uint64_t tile) {
         nch = std::min<uint64_t>(kMaxChunks, (m + tile - 1) / tile);
@@ -444,7 +408,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         uint64_t* dst = first0 ? *k : *k2;
         if (first0) {
             if (timed) HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-            launch_sort0(c, s0, wid, n, *k, *k2, shift, dmask, table, remap0, kept, lo + bits, lo + 2 * bits, dhist);
+            launch_sort0(c, s0, wid, *k, *k2, shift, dmask, table, remap0, kept, lo + bits, lo + 2 * bits, dhist);
             if (timed) HIPCK(hipEventRecord(c->ev_c0[1], c->st));
             CK(run_scan(c, OpInPlace{table}, (uint64_t)kRadix * nch, totals + 4));
             if (sweep) k_digit_bases<<<kLaterDigits, kRadix, 0, c->st>>>(dhist, dhist + kLaterDigits * kRadix);
@@ -587,7 +551,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const bool wide = m > kRadixBits;  // (k_sort0_compact<.., kWideD>, k_msd_scatter_wide)
     const uint32_t rows = wide ? nb : kRadix;  // digit rows of the table
     S0Geom s0{};
-    CK(s0_geometry(c, n, k2, &s0, wide));
+    CK(s0_geometry(c, &s0));
     const uint64_t nch = s0.ncol;
     CK(grow(c->rtable, sizeof(uint64_t) * rows * kMaxChunks));
     CK(grow(c->kept, sizeof(uint64_t) * 2 * kMaxChunks));
@@ -605,18 +569,8 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const int shift = lo + L;  // the top digit of the key
     const uint32_t dmask = nb - 1u;
 
-    // the split first-pass output (II_S0_SPLIT=1): u32 records, then their digits, in *k2
-    S0Split sp;
-    const char* sk = getenv("II_S0_SPLIT");
-    if (sk && !strcmp(sk, "1")) {
-        sp.out = wide ? 2 : 1;
-        sp.rec32 = reinterpret_cast<uint32_t*>(*k2);
-        sp.dig = sp.rec32 + (s0.half ? 2 * n : n);  // (rec2 holds 8n bytes, 16n paired)
-        sp.pack_f = F;
-        sp.pack_low = (1u << L) - 1u;
-    }
     HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-    launch_sort0(c, s0, wid, n, *k, *k2, shift, dmask, table, remap0, kept, 0, 0, nullptr, wide, sp);
+    launch_sort0(c, s0, wid, *k, *k2, shift, dmask, table, remap0, kept, 0, 0, nullptr, wide);
     HIPCK(hipEventRecord(c->ev_c0[1], c->st));
     CK(run_scan(c, OpInPlace{table}, (uint64_t)rows * nch, totals + 4));
     k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);
@@ -628,20 +582,10 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
     uint32_t* out32 = reinterpret_cast<uint32_t*>(*k);
     constexpr int NTs = kScatterThreads, ITs = kScatterItems;
-    if (sp.out == 1) {
-        k_msd_scatter<NTs, ITs, kRadix, uint8_t><<<(uint32_t)nch, NTs, 0, c->st>>>(
-            nullptr, sp.rec32, static_cast<const uint8_t*>(sp.dig), out32, shift, m, (uint32_t)nch, table, kept, pad, F,
-            sp.pack_low);
-    } else if (sp.out == 2) {
-        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512, uint16_t>
-                 : m <= 10 ? k_msd_scatter<NTs, ITs, 1024, uint16_t> : k_msd_scatter<NTs, ITs, kMsdMax, uint16_t>;
-        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(nullptr, sp.rec32, static_cast<const uint16_t*>(sp.dig), out32, shift, m,
-                                             (uint32_t)nch, table, kept, pad, F, sp.pack_low);
-    } else if (wide) {
+    if (wide) {
         auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
                                                                    : k_msd_scatter<NTs, ITs, kMsdMax>;
-        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, nullptr, nullptr, out32, shift, m, (uint32_t)nch, table, kept, pad, F,
-                                             (1u << L) - 1u);
+        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
     } else {
         k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
             *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept,
@@ -654,10 +598,9 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const uint64_t n_in = n;
     n = t47[0];
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
-    const uint64_t kept_b = sp.out ? 4 + sp.out : 8;  // bytes of a kept record between the first pass and the MSD
-    c->c0_bytes = 8 * n_in + kept_b * n;
+    c->c0_bytes = 8 * n_in + 8 * n;
     *n_out = n;
-    if (ev) c->sc_bytes[c->n_sc++] = (kept_b + 4) * n;
+    if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
     *passes = 1;
     if (n == 0) return II_OK;
     // per-bucket digit counts of the two LSD passes -> bases
@@ -792,6 +735,7 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     ii_ctx* c = new ii_ctx();
     c->dev = device;
     HIPCK(hipSetDevice(device));
+    HIPCK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
     HIPCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HIPCK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
@@ -1824,7 +1768,9 @@ static int merge_sources(ii_ctx* c, K** src, K** dst, std::vector<uint64_t> len,
             CK(grow(c->moff, sizeof(uint64_t) * (tiles + 1)));
             uint64_t* split = P_<uint64_t>(c->moff);
             k_merge_partition<K><<<grid_for(tiles + 1), kBlock, 0, c->st>>>(*src, mr, split);
-            k_merge_tiles<K><<<(uint32_t)tiles, kMergeNT, 0, c->st>>>(*src, *dst, mr, split);
+            // persistent workgroups: a few per CU (LDS: 2 tiles of K)
+            const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->ncu * (sizeof(K) == 8 ? 4 : 8));
+            k_merge_tiles<K><<<(uint32_t)grid, kMergeNT, 0, c->st>>>(*src, *dst, mr, split);
             HIPCK(hipGetLastError());
         }
         std::swap(*src, *dst);

@@ -1453,7 +1453,10 @@ __global__ __launch_bounds__(kBlock) void k_letter_start(const uint64_t* __restr
 // KiB: one 1024-thread workgroup per CU; covering only half of it doubled
 // the sort time, and a 64 KiB direct-mapped cache of kept records — two
 // workgroups per CU — kept 0.50 T records instead of 0.34 T: the frequent
-// words' entries were evicted by the rare ones).  The kept records' later
+// words' entries were evicted by the rare ones; round 4: two 512-thread
+// workgroups per CU, each reading the range and deduplicating one half of the
+// hot slots with a 64 KiB bitmap, 3.9 -> 8.0 ms; the kept records written as
+// u32 + top digit instead of u64, 3.9 -> 4.1 ms and the MSD scatter no faster).  The kept records' later
 // radix digits are counted here too (dhist, global atomics per workgroup):
 // the onesweep passes that follow need only those global counts.
 constexpr uint32_t kDedupWords = (uint32_t)(kHotSlots / 32);
@@ -1465,42 +1468,22 @@ constexpr uint32_t kCMaxGroup = 1024;           // K1b chunks per workgroup (LDS
 constexpr int kLaterDigits = 2;                 // digits counted for the onesweep passes
 // LDS: 16 KiB counts + 128 KiB bitmap + 4 KiB offsets + 2 KiB later digits: one workgroup per CU
 
-// kHalf: TWO 512-thread workgroups per range of chunks, each with a 64 KiB
-// bitmap of half the hot level — half 0 keeps the records of hot slots [0,
-// 2^19), half 1 those of [2^19, 2^20) and of the big table — so that two
-// workgroups fit a CU (one barrier stalls while the other works).  Both read
-// the range's records (the pair are blocks b and b + 8: one XCD under the
-// observed round-robin placement, so the second read mostly hits its L2 —
-// speed only); each writes its kept records to an output region of its own
-// (half 1: past the first T records) and its digit counts to its own table
-// column (col = half * ranges + range).  Equal keys share a slot, hence a
-// half, hence a workgroup that keeps them in file order: the stable passes
-// that follow keep that order whatever the column order interleaves.
 // kWideD: top digits of up to kMsdMaxBits bits (the packed sort's wide MSD
-// split, k_msd_scatter_wide): one count row of kMsdMax digits shared by the
-// waves (16 per-wave rows would not fit beside the bitmap); rows d <= dmask.
-// kOut (the packed sort): 0 = u64 records to kout; 1 / 2 = split — the u32
-// record (key & pack_low) << pack_f | id to kout32 and its top digit (u8 / u16)
-// to kdig, at the same index (k_msd_scatter reads 5 / 6 bytes a record).
-template <bool kWid, bool kHalf = false, bool kWideD = false, int kOut = 0, int NT = kHalf ? kCBlock / 2 : kCBlock>
-__global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
+// split, k_msd_scatter): one count row of kMsdMax digits shared by the waves
+// (16 per-wave rows would not fit beside the bitmap); rows d <= dmask.
+template <bool kWid, bool kWideD = false>
+__global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
                                                            const uint64_t* __restrict__ voff, uint32_t nch_in,
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
                                                            uint32_t nchunks, uint64_t* __restrict__ table,
                                                            const uint32_t* __restrict__ remap,
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
                                                            int shift1, int shift2, uint64_t* __restrict__ dhist,
-                                                           const uint32_t* __restrict__ cf,
-                                                           uint32_t nranges = 0, uint64_t half_off = 0,
-                                                           uint32_t* __restrict__ kout32 = nullptr,
-                                                           void* __restrict__ kdig = nullptr, int pack_f = 0,
-                                                           uint32_t pack_low = 0) {
-    constexpr int NWv = NT / 64;
-    constexpr int kTile = kS0Items * NT;
-    constexpr uint32_t kBmWords = kHalf ? kDedupWords / 2 : kDedupWords;
-    static_assert(!(kHalf && kWideD), "one or the other");
-    // (kHalf: wave pairs share a row, so two workgroups fit 160 KiB)
-    constexpr int kCntRows = kWideD ? 1 : kHalf ? NWv / 2 : NWv;
+                                                           const uint32_t* __restrict__ cf) {
+    constexpr int NT = kCBlock, NWv = kCWaves;
+    constexpr int kTile = kCTile;
+    constexpr uint32_t kBmWords = kDedupWords;
+    constexpr int kCntRows = kWideD ? 1 : NWv;
     constexpr int kCntD = kWideD ? kMsdMax : kRadix;
     __shared__ uint32_t cnt[kCntRows][kCntD];
     __shared__ uint32_t bm[kBmWords];
@@ -1510,12 +1493,7 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
     __shared__ uint32_t s_wtot[2][NWv];          // per tile parity: one barrier per tile
     __shared__ uint32_t s_last[2];               // per tile parity: file of the tile's last record
     const int w = wave_id(), l = lane_id();
-    // kHalf: block b -> range (b / 16) * 8 + b % 8, half (b / 8) % 2; its table column half * ranges + range
-    const uint32_t range = kHalf ? (blockIdx.x / 16) * 8 + blockIdx.x % 8 : blockIdx.x;
-    const uint32_t half = kHalf ? (blockIdx.x / 8) % 2 : 0u;
-    if (kHalf && range >= nranges) return;  // (a spare block of the grid rounded to 16)
-    const uint32_t col = kHalf ? half * nranges + range : blockIdx.x;
-    const uint32_t c0 = range * group, ng = c0 + group < nch_in ? group : nch_in - c0;
+    const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
     for (int i = threadIdx.x; i < kCntRows * kCntD; i += NT) (&cnt[0][0])[i] = 0;
     for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += NT) (&s_later[0][0])[i] = 0;
     for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = 0;
@@ -1532,8 +1510,7 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
     uint32_t gadj = chunk_rot(c0);                   // rot(chunk) - chunk start
     uint64_t gbase = (uint64_t)c0 * cap;
     uint32_t gfid = ng ? s_cfid[0] : ~0u;            // narrow chunk's file (~0: u64 records)
-    uint64_t o = lo + (kHalf && half ? half_off : 0ull);  // next output position
-    const uint64_t o0 = o;
+    uint64_t o = lo;  // next output position
     // The next tile's records are loaded while this one is written: issued
     // after this tile's remap gathers have been consumed (vmcnt is in order, so
     // a prefetch issued before them would make the gathers wait for it).
@@ -1591,11 +1568,9 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
         for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
-            if (kHalf) ok = ok && (uint32_t)(slot >= (kHotSlots >> 1)) == half;  // (big-table slots: half 1)
             if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
-                const uint32_t bs = kHalf ? (uint32_t)slot & (uint32_t)(kHotSlots / 2 - 1) : (uint32_t)slot;
-                const uint32_t bit = 1u << (bs & 31);
-                ok = !(atomicOr(&bm[bs >> 5], bit) & bit);
+                const uint32_t bit = 1u << (slot & 31);
+                ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
             }
             const uint64_t b = __ballot(ok);
             pos[k] = wcount + (uint32_t)__popcll(b & lt);
@@ -1629,15 +1604,8 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
         for (int k = 0; k < kS0Items; k++) {
             if ((keep >> k) & 1u) {
                 const uint64_t r = raw[k];
-                if constexpr (kOut == 0) {
-                    st_nt(kout + o + wbase + pos[k], r);
-                } else {
-                    const uint64_t q = o + wbase + pos[k];
-                    kout32[q] = (((uint32_t)(r >> 32) & pack_low) << pack_f) | (uint32_t)r;
-                    if constexpr (kOut == 1) static_cast<uint8_t*>(kdig)[q] = (uint8_t)((r >> shift) & dmask);
-                    else static_cast<uint16_t*>(kdig)[q] = (uint16_t)((r >> shift) & dmask);
-                }
-                atomicAdd(&cnt[kWideD ? 0 : kHalf ? w >> 1 : w][(uint32_t)(r >> shift) & dmask], 1u);
+                st_nt(kout + o + wbase + pos[k], r);
+                atomicAdd(&cnt[kWideD ? 0 : w][(uint32_t)(r >> shift) & dmask], 1u);
                 if (dhist) {
                     atomicAdd(&s_later[0][(uint32_t)(r >> shift1) & dmask], 1u);
                     atomicAdd(&s_later[1][(uint32_t)(r >> shift2) & dmask], 1u);
@@ -1651,7 +1619,7 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
         uint32_t tt = 0;
 #pragma unroll
         for (int ww = 0; ww < kCntRows; ww++) tt += cnt[ww][d];
-        table[(uint64_t)d * nchunks + col] = tt;
+        table[(uint64_t)d * nchunks + blockIdx.x] = tt;
         if (kWideD) continue;  // (no later digits: the packed sort only)
         if (dhist) {
             if (s_later[0][d]) atomicAdd((unsigned long long*)&dhist[d], (unsigned long long)s_later[0][d]);
@@ -1659,8 +1627,8 @@ __global__ __launch_bounds__(NT, 4) void k_sort0_compact(const uint64_t* __restr
         }
     }
     if (threadIdx.x == 0) {
-        kept[col] = o - o0;
-        kept[kMaxChunks + col] = o0;
+        kept[blockIdx.x] = o - lo;
+        kept[kMaxChunks + blockIdx.x] = lo;
     }
 }
 
@@ -2439,46 +2407,86 @@ __global__ __launch_bounds__(kBlock) void k_merge_partition(const K* __restrict_
     split[tile] = merge_corank(A, mr.na[p], A + mr.na[p], mr.nb[p], k);
 }
 
+// Persistent tile loop: workgroup b takes tiles b, b + grid, ...; the next
+// tile's two slices are loaded into registers while this one is merged in LDS
+// (a workgroup with one short-lived tile waited out every load: 0.31 ms per
+// round of 5·10^7 u64 records, 2.7 TB/s).
 template <class K>
 __global__ __launch_bounds__(kMergeNT) void k_merge_tiles(const K* __restrict__ src, K* __restrict__ dst, MergeRound mr,
                                                           const uint64_t* __restrict__ split) {
     __shared__ K s_in[kMergeTile];
     __shared__ K s_out[kMergeTile];
-    const uint32_t tile = blockIdx.x;
-    const uint32_t p = merge_pair_of(mr, tile);
-    const uint64_t na = mr.na[p], nb = mr.nb[p];
-    const uint64_t k0 = (uint64_t)(tile - mr.tile0[p]) * kMergeTile;
-    const uint64_t k1 = k0 + kMergeTile < na + nb ? k0 + kMergeTile : na + nb;
-    const uint64_t i0 = split[tile];
-    const uint64_t i1 = tile + 1 == mr.tile0[p + 1] ? na : split[tile + 1];  // (the pair's last tile ends at na)
-    const uint64_t j0 = k0 - i0, j1 = k1 - i1;
-    const uint32_t la = (uint32_t)(i1 - i0), lb = (uint32_t)(j1 - j0), n = la + lb;
-    const K* A = src + mr.a[p];
-    const K* B = A + na;
-    for (uint32_t x = threadIdx.x; x < n; x += kMergeNT) s_in[x] = x < la ? A[i0 + x] : B[j0 + (x - la)];
-    __syncthreads();
-    // this thread's outputs [q0, q0 + IT): its own merge path inside the tile, then a sequential merge
-    const uint32_t q0 = threadIdx.x * kMergeIT;
-    if (q0 < n) {
-        uint32_t lo = q0 > lb ? q0 - lb : 0, hi = q0 < la ? q0 : la;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_in[mid] <= s_in[la + q0 - 1 - mid]) lo = mid + 1;
-            else hi = mid;
-        }
-        uint32_t ia = lo, ib = q0 - lo;
+    const uint32_t ntiles = mr.tile0[mr.npairs];
+    struct Slice {
+        uint32_t p, la, lb, n;
+        uint64_t k0;
+    };
+    auto slice_of = [&](uint32_t tile) {
+        Slice sl;
+        sl.p = merge_pair_of(mr, tile);
+        const uint64_t na = mr.na[sl.p], nb = mr.nb[sl.p];
+        sl.k0 = (uint64_t)(tile - mr.tile0[sl.p]) * kMergeTile;
+        const uint64_t k1 = sl.k0 + kMergeTile < na + nb ? sl.k0 + kMergeTile : na + nb;
+        const uint64_t i0 = split[tile];
+        const uint64_t i1 = tile + 1 == mr.tile0[sl.p + 1] ? na : split[tile + 1];  // (the pair's last tile ends at na)
+        sl.la = (uint32_t)(i1 - i0);
+        sl.lb = (uint32_t)((k1 - i1) - (sl.k0 - i0));
+        sl.n = sl.la + sl.lb;
+        return sl;
+    };
+    // this thread's elements x = q * kMergeNT + t of a tile: its left slice, then its right slice
+    K pre[kMergeIT];
+    auto load = [&](uint32_t tile, const Slice& sl) {
+        const K* A = src + mr.a[sl.p];
+        const K* B = A + mr.na[sl.p];
+        const uint64_t i0 = split[tile], j0 = sl.k0 - i0;
 #pragma unroll
         for (int q = 0; q < kMergeIT; q++) {
-            if (q0 + q >= n) break;
-            const bool takeA = ib >= lb || (ia < la && s_in[ia] <= s_in[la + ib]);
-            s_out[q0 + q] = takeA ? s_in[ia] : s_in[la + ib];
-            ia += takeA;
-            ib += !takeA;
+            const uint32_t x = q * kMergeNT + threadIdx.x;
+            pre[q] = x < sl.la ? A[i0 + x] : x < sl.n ? B[j0 + (x - sl.la)] : (K)0;
         }
+    };
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    Slice sl = slice_of(tile);
+    load(tile, sl);
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < kMergeIT; q++) s_in[q * kMergeNT + threadIdx.x] = pre[q];
+        __syncthreads();  // (also: every thread has stored the last tile's s_out)
+        const uint32_t next = tile + gridDim.x;
+        Slice nsl{};
+        if (next < ntiles) {
+            nsl = slice_of(next);
+            load(next, nsl);
+        }
+        // this thread's outputs [q0, q0 + IT): its own merge path inside the tile, then a sequential merge
+        const uint32_t la = sl.la, lb = sl.lb, n = sl.n;
+        const uint32_t q0 = threadIdx.x * kMergeIT;
+        if (q0 < n) {
+            uint32_t lo = q0 > lb ? q0 - lb : 0, hi = q0 < la ? q0 : la;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_in[mid] <= s_in[la + q0 - 1 - mid]) lo = mid + 1;
+                else hi = mid;
+            }
+            uint32_t ia = lo, ib = q0 - lo;
+#pragma unroll
+            for (int q = 0; q < kMergeIT; q++) {
+                if (q0 + q >= n) break;
+                const bool takeA = ib >= lb || (ia < la && s_in[ia] <= s_in[la + ib]);
+                s_out[q0 + q] = takeA ? s_in[ia] : s_in[la + ib];
+                ia += takeA;
+                ib += !takeA;
+            }
+        }
+        __syncthreads();
+        K* out = dst + mr.a[sl.p] + sl.k0;
+        for (uint32_t x = threadIdx.x; x < n; x += kMergeNT) out[x] = s_out[x];
+        if (next >= ntiles) return;  // (workgroup-uniform)
+        tile = next;
+        sl = nsl;
     }
-    __syncthreads();
-    K* out = dst + mr.a[p] + k0;
-    for (uint32_t x = threadIdx.x; x < n; x += kMergeNT) out[x] = s_out[x];
 }
 
 }  // namespace ii

@@ -7,7 +7,6 @@
 // the per-chunk results, and a third kernel re-reads its chunk and writes.
 // Chunks are processed tile by tile in order, so the radix sort is stable.
 #pragma once
-#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -398,19 +397,16 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin,
 // digits spread over the threads (R / NT consecutive digits each; top digits
 // up to kMsdMaxBits: the F = 19 share of configs[4] needs m = 10) and the tile
 // held as the u32 records plus u16 digits, per-wave counts in u16 (a tile
-// holds < 2^16 records): 53 / 74 KiB of LDS at R = 256 / 1024.
-// D = void: the first pass left u64 records (key << 32 | id); otherwise it
-// left them split (k_sort0_compact kOut): the u32 records already packed in
-// kin32 and their top digits (D = u8 or u16) in kdig — 5 or 6 bytes a record
-// read instead of 8.
-template <int NT, int IT, int R, class D = void>
-__global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ kin32,
-                                                    const D* __restrict__ kdig, uint32_t* __restrict__ kout32,
+// holds < 2^16 records): 62 / 74 / 100 KiB of LDS at R = 512 / 1024 / 2048.
+// (Round 4, measured and dropped: the first pass writing the records already
+// split — u32 + a u8 top digit, 5 bytes read here instead of 8 — made the
+// first pass 0.2 ms slower and this pass no faster at config3.)
+template <int NT, int IT, int R>
+__global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__ kin, uint32_t* __restrict__ kout32,
                                                     int shift, int dbits, uint32_t nchunks,
                                                     const uint64_t* __restrict__ table,
                                                     const uint64_t* __restrict__ kept,
                                                     const uint64_t* __restrict__ pad, int pack_f, uint32_t pack_low) {
-    constexpr bool kSplit = !std::is_void<D>::value;
     constexpr int NW = NT / 64;
     constexpr int kTileN = NT * IT;
     constexpr int DPT = R / NT > 0 ? R / NT : 1;  // digits per thread (threads t < R own one when R < NT)
@@ -435,14 +431,9 @@ __global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const uint64_t idx = wb + (uint64_t)k * 64;
-            if constexpr (kSplit) {
-                nrec[k] = idx < hi ? kin32[idx] : 0u;
-                ndg[k] = idx < hi ? (uint32_t)kdig[idx] : 0u;
-            } else {
-                const uint64_t x = idx < hi ? kin[idx] : 0ull;
-                nrec[k] = (((uint32_t)(x >> 32) & pack_low) << pack_f) | (uint32_t)x;
-                ndg[k] = (uint32_t)(x >> shift) & dmask;
-            }
+            const uint64_t x = idx < hi ? kin[idx] : 0ull;
+            nrec[k] = (((uint32_t)(x >> 32) & pack_low) << pack_f) | (uint32_t)x;
+            ndg[k] = (uint32_t)(x >> shift) & dmask;
         }
     };
     if (lo < hi) load_tile(lo);
@@ -877,7 +868,10 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
 // the bucket's first tile, which publishes an inclusive prefix at once.
 // Digit d of bucket h starts at the bucket's padded start + dbase[h * dstride + d].
 // (launch bound of 6 waves per SIMD: without one the compiler spent 256 VGPRs
-// with spills, one workgroup per CU, 2.4x slower than k_onesweep)
+// with spills, one workgroup per CU, 2.4x slower than k_onesweep.  Round 4,
+// dropped: a workgroup claiming two tiles and loading both up front — its
+// second tile publishes only after the first is written, and the look-backs
+// behind it wait in a chain: 1.6 -> 115 ms per pass.)
 template <int NT, int IT, int kLbPer = 2>
 __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restrict__ kin, uint64_t ncap,
                                                      uint32_t* __restrict__ kout,

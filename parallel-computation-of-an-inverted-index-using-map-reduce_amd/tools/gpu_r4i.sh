@@ -18,8 +18,8 @@ print('value=%.1f verified=%s packed=%s ms/step=%.2f sort_phase=%.4f sort0=%.3f 
 }
 echo "== tests" && \
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-    -k "first_pass_forms or packed_sort or tiny_shapes or owner_sort or logical_shards or export_after_reduce or two_ranks" > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc = 0 ] && \
-bash $T/gpu_env_ab.sh $TAG 10e9 10 - II_S0_HALF=1 II_S0_SPLIT=1 "II_S0_HALF=1 II_S0_SPLIT=1" - && \
+    -k "first_pass_forms or sweep_two_tiles or packed_sort or tiny_shapes or owner_sort or logical_shards or export_after_reduce or two_ranks" > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc = 0 ] && \
+bash $T/gpu_env_ab.sh $TAG 10e9 10 - II_S0_HALF=1 II_S0_SPLIT=1 "II_S0_HALF=1 II_S0_SPLIT=1" II_SWEEP_TPW=2 - && \
 r7 base II_NONE=1 && r7 split II_S0_SPLIT=1
 [ $? = 0 ] && echo "== exchange timing" && timeout -k 10 300 python $T/exchange_timing.py 1.25e9 8 3 1 > $OUT/xchg.json 2> $OUT/xchg.err && tail -c 700 $OUT/xchg.json && \
 echo "== rocprof exchange timing (G=8 owner import kernels)" && \

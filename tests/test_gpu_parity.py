@@ -457,17 +457,12 @@ def test_packed_sort_forms_vs_oracle():
 
 
 @pytest.mark.parametrize("env", [{"II_PACKED_M": "9"}, {"II_PACKED_M": "10"}, {"II_PACKED_M": "11"},
-                                 {"II_S0_HALF": "1"}, {"II_S0_HALF": "1", "II_PACKED_SORT": "0"},
-                                 {"II_S0_HALF": "1", "II_SORT_KEYS": "lexid"}, {"II_S0_SPLIT": "1"},
-                                 {"II_S0_SPLIT": "1", "II_PACKED_M": "10"}, {"II_S0_SPLIT": "1", "II_S0_HALF": "1"}])
-def test_sort_first_pass_forms_vs_oracle(env):
+                                 {"II_PACKED_M": "10", "II_SORT_KEYS": "lexid"}])
+def test_wide_top_digit_vs_oracle(env):
     """The token sort's wide top digit (II_PACKED_M forces m top bits: the
-    wide MSD split k_msd_scatter_wide and k_sort0_compact's wide count row, the
-    form configs[4]'s F = 19 share takes) and the paired first pass (II_S0_HALF:
-    two half-bitmap workgroups per range, k_sort0_compact<.., kHalf>) and its
-    split output (II_S0_SPLIT: u32 records + top digits, k_msd_scatter) in the
-    packed and u64 sorts and with both key kinds, against the oracle; ids
-    spread to 22 bits and 700 files of very different sizes."""
+    wide MSD split k_msd_scatter and k_sort0_compact's wide count row, the form
+    configs[4]'s F = 19 share takes) with both key kinds, against the oracle;
+    ids spread to 22 bits and 700 files of very different sizes."""
     t, off = ii_ctypes.zipf_corpus(48_000_000, 700, 3_000_000, 29, threads=8)
     off = off.tolist()
     ids = [6007 * i for i in range(700)]
@@ -480,7 +475,7 @@ def test_sort_first_pass_forms_vs_oracle(env):
                 ix.reduce()
                 assert_same(ix.letters(), exp, "%s rep %d" % (env, rep))
             st = ix.stats()
-            assert st.sort_packed == (0 if env.get("II_PACKED_SORT") == "0" else 1)
+            assert st.sort_packed == 1
             assert st.sort_bytes > 0
     finally:
         for k in env:
