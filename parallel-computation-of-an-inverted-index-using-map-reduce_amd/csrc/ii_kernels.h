@@ -21,7 +21,7 @@ namespace ii {
 // ---------------------------------------------------------------- constants
 constexpr uint64_t kChunk = 16384;  // bytes of text per K1 chunk (one wave each, see "K1 chunks")
 constexpr int kMaxWord = 299;      // MAX_WORD - 1 letters (main.c:7, 105)
-constexpr int kMaxProbe = 1 << 14;
+constexpr int kMaxProbe = 1 << 12;  // big-table probe bound (load <= 1/2 enforced by the host): past it, C_OVERFLOW
 
 constexpr uint32_t kSlotNone = 0xFFFFFFFFu;  // token with no letters (dropped, main.c:113)
 
@@ -146,6 +146,12 @@ __device__ __forceinline__ uint32_t table_find(const Table& t, uint64_t key, uin
         if (kb == 0ull) kb = table_claim(t, s, key, pos);
         if (kb == key) return (uint32_t)s;
         h = (h + 1) & t.big_mask;
+        // a table another lane found full: this attempt is void (the host regrows the table and maps
+        // again), so leave at once — a full table otherwise costs every new word kMaxProbe probes
+        // (3.4 s instead of 27 ms for the first map of configs[4]'s rank-7 share, 6.7·10^6 words)
+        if ((probe & 15) == 15 &&
+            (__hip_atomic_load(&t.counters[C_OVERFLOW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull))
+            return 0;
     }
     atomicOr((unsigned long long*)&t.counters[C_OVERFLOW], 1ull);
     return 0;
