@@ -196,7 +196,8 @@ int ii_export_plan_ranges(ii_ctx *ctx, int nparts, const int *letter_lo, const i
 int ii_export(ii_ctx *ctx, int nparts, void *d_send, const uint64_t *send_off);
 /* ii_import: segment s comes from source s (0 .. nparts-1, any order of file
  * ids across sources), and every file id belongs to ONE source — files are
- * sharded, not replicated (main.c:300-323 gives each file one mapper). */
+ * sharded, not replicated (main.c:300-323 gives each file one mapper).
+ * 1 <= nparts <= II_MAX_PARTS, else II_ERR_ARG. */
 int ii_import(ii_ctx *ctx, int nparts, const void *d_recv, const uint64_t *recv_off, uint32_t id_bound);
 
 /* Text of <letter>.txt (letter 0..25 = 'a'..'z'), valid until the next call. */

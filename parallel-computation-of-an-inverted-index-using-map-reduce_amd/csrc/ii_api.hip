@@ -52,6 +52,7 @@ struct ii_ctx {
     uint32_t nfiles = 0;
     uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df)
     bool fid_ident = true;  // the mapped files' id0s are 0, 1, 2, ... (K1's shard-local file index == id0)
+    IdDigitsTh dth{};       // K3's posting bytes by file index (pair_bytes)
     DBuf fstart, fid;
     std::vector<uint64_t> h_fstart;  // host copies of the mapped files' starts / ids
     std::vector<uint32_t> h_fid;
@@ -617,7 +618,11 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
-    k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
+    const char* shm = getenv("II_SEGHIST");  // (A/B knob: 0 plain, 1 wave groups, 2 four copies)
+    const int shmode = shm ? atoi(shm) : 1;
+    auto* shk = shmode == 0 ? k_seg_hist<kSweepThreads, kSweepItems, 0>
+              : shmode == 2 ? k_seg_hist<kSweepThreads, kSweepItems, 2> : k_seg_hist<kSweepThreads, kSweepItems, 1>;
+    shk<<<hg, kSweepThreads, 0, c->st>>>(
         reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
     HIPCK(hipGetLastError());
@@ -693,14 +698,14 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             nullptr, n, reinterpret_cast<const uint32_t*>(r), c->pk_ncap, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64);
+            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64, c->dth);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
         k_uniq_sweep<false><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
             P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW,
-            fmap, u32, g64);
+            fmap, u32, g64, c->dth);
         k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     }
     // K3's look-back flags kLbTimeout instead of hanging (a predecessor tile that never
@@ -1044,6 +1049,12 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
     c->fid_ident = !nfiles || file_id0[nfiles - 1] == nfiles - 1;  // ascending ids: the last is nfiles - 1 iff all are i
     c->h_fstart.assign(file_start, file_start + nfiles);
     c->h_fid.assign(file_id0, file_id0 + nfiles);
+    for (int k = 0; k < 9; k++) {  // the first file index whose id0 + 1 >= 10^(k + 1)
+        uint64_t p10 = 10;
+        for (int j = 0; j < k; j++) p10 *= 10;
+        c->dth.t[k] = (uint32_t)(std::lower_bound(c->h_fid.begin(), c->h_fid.end(), (uint32_t)std::min<uint64_t>(p10 - 1, ~0u)) -
+                                 c->h_fid.begin());
+    }
     c->part_valid = false;
     c->text_is_input = true;
     c->collide_retries = 0;
@@ -1781,7 +1792,7 @@ static int merge_sources(ii_ctx* c, K** src, K** dst, std::vector<uint64_t> len,
 }
 
 extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64_t* recv_off, uint32_t id_bound) {
-    if (!c || nparts < 1 || !recv_off || (!d_recv && nparts)) return II_ERR_ARG;
+    if (!c || nparts < 1 || nparts > II_MAX_PARTS || !recv_off || (!d_recv && nparts)) return II_ERR_ARG;
     LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
     CK(settle_side(c));
@@ -1851,21 +1862,24 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // The pairs go to r (rec2) in every form: r2 is rec, which holds the word
     // records wrec every source's pairs are mapped through (writing records
     // there would overwrite word records later sources still read).
-    uint64_t wbase = 0, pbase = 0;
+    ImportSrc isrc;
+    memset(&isrc, 0, sizeof(isrc));
+    isrc.n = (uint32_t)nparts;
     std::vector<uint64_t> runs;
+    static_assert(kImportMaxSrc >= II_MAX_PARTS, "one import launch for every source");
+    uint64_t wbase = 0;
     for (int s = 0; s < nparts; s++) {
-        const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
-        const uint64_t* src = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
-        const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
-        if (np && use32)
-            k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
-                                                          reinterpret_cast<uint32_t*>(r) + pbase, Fid);
-        else if (np)
-            k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
-        wbase += nw;
-        pbase += np;
-        runs.push_back(np);
+        isrc.p[s] = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
+        isrc.wbase[s] = wbase;
+        isrc.pbase[s + 1] = isrc.pbase[s] + hdr[8 * s + 2];
+        wbase += hdr[8 * s + 1];
+        runs.push_back(hdr[8 * s + 2]);
     }
+    const uint32_t ig = (uint32_t)((NP + kImportPer - 1) / kImportPer);
+    if (use32)
+        k_import_pairs<true><<<ig, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, Fid);
+    else
+        k_import_pairs<false><<<ig, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, 0);
     HIPCK(hipGetLastError());
     int p1 = 0, p2 = 0;
     c->n_sc = 0;

@@ -1670,6 +1670,22 @@ __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
     return 1u + (v >= 10ull) + (v >= 100ull) + (v >= 1000ull) + (v >= 10000ull) + (v >= 100000ull) +
            (v >= 1000000ull) + (v >= 10000000ull) + (v >= 100000000ull) + (v >= 1000000000ull);
 }
+// Posting bytes of a pair by its shard-local file index f (ids ascend with f):
+// t[k - 1] = the first index whose id0 + 1 has more than k digits, so the bytes
+// (separator + digits of id0 + 1) follow from nine compares instead of a
+// gather of fmap[f] — K3 publishes its tile aggregate without waiting for
+// the gathers (configs[4]'s rank-7 share: 4.4·10^5 files, a 1.8 MB fmap that
+// misses L1 on every pair).
+struct IdDigitsTh {
+    uint32_t t[9];
+};
+__device__ __forceinline__ uint32_t pair_bytes(const uint32_t* __restrict__ fmap, const IdDigitsTh& th, uint32_t f) {
+    if (!fmap) return id_digits((uint64_t)f + 1) + 1;
+    uint32_t d = 2;
+#pragma unroll
+    for (int k = 0; k < 9; k++) d += f >= th.t[k];
+    return d;
+}
 
 // 8-bit fields -> 16-bit fields of a u64
 __device__ __forceinline__ uint64_t field8_spread(uint32_t x) {
@@ -1747,7 +1763,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
                                                        uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err,
                                                        const uint32_t* __restrict__ fmap, uint32_t* __restrict__ uniq32,
-                                                       uint32_t* __restrict__ g64) {
+                                                       uint32_t* __restrict__ g64, IdDigitsTh dth) {
     // the tile staged in LDS (scanned, then written after the look-back): u64
     // records from [1] with the record before the tile at [0], or in the packed
     // form the raw u32 records (16 KiB, 8 workgroups per CU instead of 3) and
@@ -1843,7 +1859,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
                 c8 |= 1u << (8 * q);
-                const uint32_t d = id_digits((uint64_t)file_id0(fmap, (uint32_t)r) + 1) + 1;
+                const uint32_t d = pair_bytes(fmap, dth, (uint32_t)r);
                 if (q < 2) bl += d << (16 * q);
                 else bh += d << (16 * (q - 2));
                 tcount++;
@@ -2291,15 +2307,38 @@ __global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint6
 
 // received pair -> (global lexid, id0): word k of the merged word text was
 // tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id.
-// k32: the u32 record lexid << f32 | id0 instead (the owner's sort keys fit 32 bits)
+// k32: the u32 record lexid << f32 | id0 instead (the owner's sort keys fit 32 bits).
+// All sources in one launch (ImportSrc by value): source s's np[s] pairs at
+// p[s] go to out[pbase[s] ...) (pbase[n] = all pairs); workgroup b takes
+// [b * kImportPer, + kImportPer) and finds its first source by a binary search
+// (one launch instead of one per source: 8 launches at G = 8 cost 0.28 ms of
+// launch gaps and tails per owner).
+constexpr int kImportMaxSrc = 64;  // II_MAX_PARTS
+constexpr uint32_t kImportPer = kBlock * 16;
+struct ImportSrc {
+    uint32_t n;
+    const uint64_t* p[kImportMaxSrc];
+    uint64_t wbase[kImportMaxSrc];
+    uint64_t pbase[kImportMaxSrc + 1];
+};
 template <bool k32>
-__global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restrict__ pairs, uint64_t np, uint64_t wbase,
-                                                         const uint64_t* __restrict__ wrec,
+__global__ __launch_bounds__(kBlock) void k_import_pairs(ImportSrc src, const uint64_t* __restrict__ wrec,
                                                          const uint32_t* __restrict__ remap, void* __restrict__ out,
                                                          int f32) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
-        uint64_t r = pairs[i];
-        uint64_t slot = wrec[wbase + (r >> 32)] >> 32;
+    const uint64_t b0 = (uint64_t)blockIdx.x * kImportPer;
+    const uint64_t total = src.pbase[src.n];
+    if (b0 >= total) return;
+    uint32_t lo = 0, hi = src.n - 1;  // the last source s with pbase[s] <= b0
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (src.pbase[mid] <= b0) lo = mid;
+        else hi = mid - 1;
+    }
+    uint32_t s = lo;
+    for (uint64_t i = b0 + threadIdx.x; i < b0 + kImportPer && i < total; i += kBlock) {
+        while (i >= src.pbase[s + 1]) s++;  // (a range crossing into the next source)
+        const uint64_t r = src.p[s][i - src.pbase[s]];
+        const uint64_t slot = wrec[src.wbase[s] + (r >> 32)] >> 32;
         if (k32) static_cast<uint32_t*>(out)[i] = (remap[slot] << f32) | (uint32_t)r;
         else static_cast<uint64_t*>(out)[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
     }
