@@ -618,11 +618,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
-    const char* shm = getenv("II_SEGHIST");  // (A/B knob: 0 plain, 1 wave groups, 2 four copies)
-    const int shmode = shm ? atoi(shm) : 1;
-    auto* shk = shmode == 0 ? k_seg_hist<kSweepThreads, kSweepItems, 0>
-              : shmode == 2 ? k_seg_hist<kSweepThreads, kSweepItems, 2> : k_seg_hist<kSweepThreads, kSweepItems, 1>;
-    shk<<<hg, kSweepThreads, 0, c->st>>>(
+    k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
         reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
     HIPCK(hipGetLastError());
@@ -1862,24 +1858,21 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // The pairs go to r (rec2) in every form: r2 is rec, which holds the word
     // records wrec every source's pairs are mapped through (writing records
     // there would overwrite word records later sources still read).
-    ImportSrc isrc;
-    memset(&isrc, 0, sizeof(isrc));
-    isrc.n = (uint32_t)nparts;
+    uint64_t wbase = 0, pbase = 0;
     std::vector<uint64_t> runs;
-    static_assert(kImportMaxSrc >= II_MAX_PARTS, "one import launch for every source");
-    uint64_t wbase = 0;
     for (int s = 0; s < nparts; s++) {
-        isrc.p[s] = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
-        isrc.wbase[s] = wbase;
-        isrc.pbase[s + 1] = isrc.pbase[s] + hdr[8 * s + 2];
-        wbase += hdr[8 * s + 1];
-        runs.push_back(hdr[8 * s + 2]);
+        const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
+        const uint64_t* src = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
+        const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
+        if (np && use32)
+            k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
+                                                          reinterpret_cast<uint32_t*>(r) + pbase, Fid);
+        else if (np)
+            k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
+        wbase += nw;
+        pbase += np;
+        runs.push_back(np);
     }
-    const uint32_t ig = (uint32_t)((NP + kImportPer - 1) / kImportPer);
-    if (use32)
-        k_import_pairs<true><<<ig, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, Fid);
-    else
-        k_import_pairs<false><<<ig, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, 0);
     HIPCK(hipGetLastError());
     int p1 = 0, p2 = 0;
     c->n_sc = 0;

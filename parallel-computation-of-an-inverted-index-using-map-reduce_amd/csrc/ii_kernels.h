@@ -2308,37 +2308,16 @@ __global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint6
 // received pair -> (global lexid, id0): word k of the merged word text was
 // tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id.
 // k32: the u32 record lexid << f32 | id0 instead (the owner's sort keys fit 32 bits).
-// All sources in one launch (ImportSrc by value): source s's np[s] pairs at
-// p[s] go to out[pbase[s] ...) (pbase[n] = all pairs); workgroup b takes
-// [b * kImportPer, + kImportPer) and finds its first source by a binary search
-// (one launch instead of one per source: 8 launches at G = 8 cost 0.28 ms of
-// launch gaps and tails per owner).
-constexpr int kImportMaxSrc = 64;  // II_MAX_PARTS
-constexpr uint32_t kImportPer = kBlock * 16;
-struct ImportSrc {
-    uint32_t n;
-    const uint64_t* p[kImportMaxSrc];
-    uint64_t wbase[kImportMaxSrc];
-    uint64_t pbase[kImportMaxSrc + 1];
-};
+// (One launch per source: a single launch over all sources, a by-value table
+// of source pointers indexed per element, measured 0.11 ms slower per owner.)
 template <bool k32>
-__global__ __launch_bounds__(kBlock) void k_import_pairs(ImportSrc src, const uint64_t* __restrict__ wrec,
+__global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restrict__ pairs, uint64_t np, uint64_t wbase,
+                                                         const uint64_t* __restrict__ wrec,
                                                          const uint32_t* __restrict__ remap, void* __restrict__ out,
                                                          int f32) {
-    const uint64_t b0 = (uint64_t)blockIdx.x * kImportPer;
-    const uint64_t total = src.pbase[src.n];
-    if (b0 >= total) return;
-    uint32_t lo = 0, hi = src.n - 1;  // the last source s with pbase[s] <= b0
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) / 2;
-        if (src.pbase[mid] <= b0) lo = mid;
-        else hi = mid - 1;
-    }
-    uint32_t s = lo;
-    for (uint64_t i = b0 + threadIdx.x; i < b0 + kImportPer && i < total; i += kBlock) {
-        while (i >= src.pbase[s + 1]) s++;  // (a range crossing into the next source)
-        const uint64_t r = src.p[s][i - src.pbase[s]];
-        const uint64_t slot = wrec[src.wbase[s] + (r >> 32)] >> 32;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
+        uint64_t r = pairs[i];
+        uint64_t slot = wrec[wbase + (r >> 32)] >> 32;
         if (k32) static_cast<uint32_t*>(out)[i] = (remap[slot] << f32) | (uint32_t)r;
         else static_cast<uint64_t*>(out)[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
     }

@@ -801,43 +801,26 @@ __global__ __launch_bounds__(kBlock) void k_tile_buckets(const uint32_t* __restr
     for (uint32_t i = btile[h] + threadIdx.x; i < btile[h + 1]; i += kBlock) tbk[i] = (uint16_t)h;
 }
 
-// c[d] += 1 for every valid lane's digit d, wave-wide (every lane calls it):
-// the digits of the first valid lanes are added as groups by their leaders —
-// up to three rounds, each a shuffle and a ballot — before the remaining lanes
-// add one by one.  A bucket ruled by a few frequent words (configs[4]'s rank-7
-// share: one record per file for its most frequent words) sends most lanes of a
-// wave to one counter, and same-address LDS atomics serialise (k_seg_hist 4.3
-// ms there, 8 conflict cycles per LDS instruction).
-__device__ __forceinline__ void hist_add_wave(uint32_t* c, uint32_t d, bool valid) {
-    bool left = valid;
-#pragma unroll
-    for (int round = 0; round < 3; round++) {
-        const uint64_t act = __ballot(left);
-        if (!act) return;  // (wave-uniform)
-        const int first = __builtin_ctzll(act);
-        const uint32_t dl = (uint32_t)__shfl((int)d, first, 64);
-        const uint64_t same = __ballot(left && d == dl);
-        if (lane_id() == first) atomicAdd(&c[dl], (uint32_t)__popcll(same));
-        left = left && d != dl;
-    }
-    if (left) atomicAdd(&c[d], 1u);
-}
-
 // Per-bucket counts of the two LSD digits of the packed records:
 // gh[(2 h + j) * kRadix + d] += records of bucket h whose digit j is d (digit j
 // = bits [s_j, s_j + b_j) of the u32).  A workgroup counts tiles
 // [blockIdx.x * per, + per) of the padded layout, 16-B loads (4 records a lane),
 // and adds its counts to gh whenever its tiles enter a new bucket.
-template <int NT, int IT, int kMode = 1>
+template <int NT, int IT>
 __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btile,
                                                  const uint64_t* __restrict__ bstart, uint32_t nb, uint32_t per, int s0,
                                                  int b0, int s1, int b1, uint64_t* __restrict__ gh) {
     constexpr uint32_t kTileN = NT * IT;
     static_assert(IT % 4 == 0, "16-B loads");
-    // kMode 2: four copies of each histogram, lane l adds to copy l % 4 (row stride kRadix + 1: a
-    // digit's four copies sit in four banks) — same-address lanes of a wave instruction split four ways
-    constexpr int kCopies = kMode == 2 ? 4 : 1;
-    constexpr int kStride = kMode == 2 ? kRadix + 1 : kRadix;
+    // four copies of each histogram, lane l adds to copy l % 4 (row stride kRadix + 1: a digit's four
+    // copies sit in four banks), so lanes of one wave instruction that share a digit split four ways:
+    // a bucket ruled by a few frequent words (configs[4]'s rank-7 share, one record per file of its
+    // most frequent words) sent most lanes to one counter, and same-address LDS atomics serialise
+    // (8 conflict cycles per LDS instruction there, 3 at config3): the rank-7 sort 29.7 -> 26.5 ms,
+    // config3 unchanged; grouping equal digits by ballots first (three leader rounds) instead cost
+    // config3 0.7 ms and saved rank 7 1.2 (profiles/r4m_seg_hist_ab.txt)
+    constexpr int kCopies = 4;
+    constexpr int kStride = kRadix + 1;
     __shared__ uint32_t c0s[kCopies * kStride], c1s[kCopies * kStride];
     uint32_t* c0 = c0s;
     uint32_t* c1 = c1s;
@@ -848,7 +831,7 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
     const uint32_t tend = tile + per < all ? tile + per : all;
     if (tile >= tend) return;
     for (uint32_t i = t; i < kCopies * kStride; i += NT) c0[i] = c1[i] = 0;
-    const uint32_t cofs = kMode == 2 ? (lane_id() & 3u) * kStride : 0u;
+    const uint32_t cofs = (lane_id() & 3u) * kStride;
     // bucket of the first tile: the last h with btile[h] <= tile (empty buckets share a start)
     uint32_t lo = 0, hi = nb - 1;
     while (lo < hi) {
@@ -888,11 +871,7 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
             const uint32_t r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const bool valid = idx + q < vend;
-                if constexpr (kMode == 1) {
-                    hist_add_wave(c0, (r[q] >> s0) & m0, valid);
-                    hist_add_wave(c1, (r[q] >> s1) & m1, valid);
-                } else if (valid) {
+                if (idx + q < vend) {
                     atomicAdd(&c0[cofs + ((r[q] >> s0) & m0)], 1u);
                     atomicAdd(&c1[cofs + ((r[q] >> s1) & m1)], 1u);
                 }
