@@ -583,9 +583,10 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
     uint32_t* out32 = reinterpret_cast<uint32_t*>(*k);
     constexpr int NTs = kScatterThreads, ITs = kScatterItems;
-    if (wide) {
-        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
-                                                                   : k_msd_scatter<NTs, ITs, kMsdMax>;
+    const char* mk = getenv("II_MSD256");  // (A/B knob: k_msd_scatter for 8-bit top digits too)
+    if (wide || (mk && !strcmp(mk, "1"))) {
+        auto* wk = m <= 8 ? k_msd_scatter<NTs, ITs, kRadix> : m <= 9 ? k_msd_scatter<NTs, ITs, 512>
+                 : m <= 10 ? k_msd_scatter<NTs, ITs, 1024> : k_msd_scatter<NTs, ITs, kMsdMax>;
         wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
     } else {
         k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(

@@ -6,7 +6,7 @@ steps ii_dist.exchange_and_reduce runs per rank — local reduce, plan +
 export, the exchange (device copies here; RCCL all-to-allv on a node),
 import, order + format — each timed across all G contexts.
 
-    python tools/exchange_timing.py [bytes_per_shard] [G] [steps] [interleaved]
+    python tools/exchange_timing.py [bytes_per_shard] [G] [steps] [interleaved] [corpus]
 
 interleaved = 1: shard g owns files g, g + G, g + 2G, ... (the id ranges of
 the sources overlap, as with bench.py's ii_partition shards, so the owners
@@ -33,14 +33,26 @@ def main():
     G = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     inter = len(sys.argv) > 4 and sys.argv[4] == "1"
+    # corpus (5th argument): the G shards are ii_partition's shares of ONE corpus of G * bytes_per_shard
+    # (as bench.py --gpus G lays them out: one vocabulary, size-sorted files, interleaved ids);
+    # otherwise every shard is a corpus of its own (its own seed, so its own words)
+    one = len(sys.argv) > 5 and sys.argv[5] == "corpus"
     files = 2000
     texts = []
+    if one:
+        layout = ii_ctypes.zipf_layout(nb * G, files * G, 3)
+        order, sb, se = ii_ctypes.partition([int(x) for x in (layout[1:] - layout[:-1])], G)
     for g in range(G):
-        t, off = ii_ctypes.zipf_corpus(nb, files, 1_000_000, 3 + 1000 * g, threads=16)
-        d = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
-        d[:nb].copy_(torch.from_numpy(t))
-        ids = list(range(g, G * files, G)) if inter else list(range(g * files, (g + 1) * files))
-        texts.append((d, off[:-1].tolist(), ids))
+        if one:
+            ids = sorted(order[sb[g]:se[g]])
+            t, off = ii_ctypes.zipf_shard(nb * G, files * G, 1_000_000, 3, ids, threads=16)
+        else:
+            t, off = ii_ctypes.zipf_corpus(nb, files, 1_000_000, 3 + 1000 * g, threads=16)
+            ids = list(range(g, G * files, G)) if inter else list(range(g * files, (g + 1) * files))
+        n = int(off[-1])
+        d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        d[:n].copy_(torch.from_numpy(t[:n]))
+        texts.append((d, off[:-1].tolist(), ids, n))
     torch.cuda.synchronize()
     idxs = [ii_ctypes.Index(0) for _ in range(G)]
     res = []
@@ -53,8 +65,8 @@ def main():
 
         for g, ix in enumerate(idxs):
             t0 = time.perf_counter()
-            d, fs, ids = texts[g]
-            ix.map_device(d.data_ptr(), nb, fs, ids)
+            d, fs, ids, n = texts[g]
+            ix.map_device(d.data_ptr(), n, fs, ids)
             lap("map", t0)
             t0 = time.perf_counter()
             ix.reduce_local()
@@ -94,7 +106,7 @@ def main():
             res.append(ph)
     avg = {k: round(sum(r[k] for r in res) / len(res), 2) for k in res[0]}
     avg["per_shard_ms"] = {k: round(v / G, 3) for k, v in avg.items() if k != "exchange_bytes"}
-    print(json.dumps({"G": G, "bytes_per_shard": nb, "interleaved_ids": inter, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
+    print(json.dumps({"G": G, "bytes_per_shard": nb, "interleaved_ids": inter or one, "one_corpus": one, "id_sort": bool(os.environ.get("II_IMPORT_ID_SORT")),
                       "phases_ms_all_shards": avg}))
     for ix in idxs:
         ix.close()
