@@ -182,7 +182,7 @@ def pmc_traffic(build, shape):
 
 # the kernels of the sort + segmented-reduce phase (K2 token sort + K3), by rocprof name prefix
 # (prefixes: the template arguments that follow vary with the build, e.g. the key type)
-PHASE_KERNELS = ("ii::k_sort0_compact", "ii::k_radix_scatter<false, 512, 16, true", "ii::k_seg_hist",
+PHASE_KERNELS = ("ii::k_sort0_compact", "ii::k_radix_scatter<false, 512, 16, true", "ii::k_msd_scatter", "ii::k_seg_hist",
                  "ii::k_onesweep", "ii::k_uniq_sweep", "ii::k_radix_scatter<false, 512, 16, false")
 
 

@@ -583,10 +583,9 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
     uint32_t* out32 = reinterpret_cast<uint32_t*>(*k);
     constexpr int NTs = kScatterThreads, ITs = kScatterItems;
-    const char* mk = getenv("II_MSD256");  // (A/B knob: k_msd_scatter for 8-bit top digits too)
-    if (wide || (mk && !strcmp(mk, "1"))) {
-        auto* wk = m <= 8 ? k_msd_scatter<NTs, ITs, kRadix> : m <= 9 ? k_msd_scatter<NTs, ITs, 512>
-                 : m <= 10 ? k_msd_scatter<NTs, ITs, 1024> : k_msd_scatter<NTs, ITs, kMsdMax>;
+    if (wide) {  // (for 8-bit top digits k_msd_scatter<.., 256> measured 0.1 ms slower than k_radix_scatter<kPack>)
+        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
+                          : k_msd_scatter<NTs, ITs, kMsdMax>;
         wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
     } else {
         k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
@@ -1859,20 +1858,31 @@ extern "C" int ii_import(ii_ctx* c, int nparts, const void* d_recv, const uint64
     // The pairs go to r (rec2) in every form: r2 is rec, which holds the word
     // records wrec every source's pairs are mapped through (writing records
     // there would overwrite word records later sources still read).
-    uint64_t wbase = 0, pbase = 0;
+    static_assert(kImportMaxSrc >= II_MAX_PARTS, "one import launch for every source");
+    ImportSrc isrc;
+    memset(&isrc, 0, sizeof(isrc));
+    isrc.n = (uint32_t)nparts;
     std::vector<uint64_t> runs;
+    uint64_t wbase = 0, pbase = 0, blocks = 0;
     for (int s = 0; s < nparts; s++) {
         const uint64_t nw = hdr[8 * s + 1], np = hdr[8 * s + 2];
-        const uint64_t* src = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
-        const uint32_t g = (uint32_t)std::min<uint64_t>(8192, grid_for(np));
-        if (np && use32)
-            k_import_pairs<true><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap),
-                                                          reinterpret_cast<uint32_t*>(r) + pbase, Fid);
-        else if (np)
-            k_import_pairs<false><<<g, kBlock, 0, c->st>>>(src, np, wbase, wrec, P_<uint32_t>(c->remap), r + pbase, 0);
+        isrc.p[s] = (const uint64_t*)((const uint8_t*)d_recv + recv_off[s] + 64);
+        isrc.np[s] = np;
+        isrc.wbase[s] = wbase;
+        isrc.pbase[s] = pbase;
+        isrc.bstart[s] = (uint32_t)blocks;
+        blocks += (np + kImportPer - 1) / kImportPer;
         wbase += nw;
         pbase += np;
         runs.push_back(np);
+    }
+    if (blocks >= (1ull << 31)) return II_ERR_NOMEM;
+    isrc.bstart[nparts] = (uint32_t)blocks;
+    if (blocks) {
+        if (use32)
+            k_import_pairs<true><<<(uint32_t)blocks, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, Fid);
+        else
+            k_import_pairs<false><<<(uint32_t)blocks, kBlock, 0, c->st>>>(isrc, wrec, P_<uint32_t>(c->remap), r, 0);
     }
     HIPCK(hipGetLastError());
     int p1 = 0, p2 = 0;

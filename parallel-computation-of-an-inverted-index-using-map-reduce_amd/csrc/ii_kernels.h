@@ -2308,18 +2308,57 @@ __global__ void k_export_header(uint64_t* __restrict__ h, uint64_t nwords, uint6
 // received pair -> (global lexid, id0): word k of the merged word text was
 // tokenised into wrec[k] = slot << 32; remap gives the owner's lexicographic id.
 // k32: the u32 record lexid << f32 | id0 instead (the owner's sort keys fit 32 bits).
-// (One launch per source: a single launch over all sources, a by-value table
-// of source pointers indexed per element, measured 0.11 ms slower per owner.)
+// All sources in one launch: source s's np pairs at p[s] go to out[pbase[s] ...)
+// and get workgroups [bstart[s], bstart[s + 1]) of kImportPer pairs each, so a
+// workgroup reads ONE source (its index found by a uniform binary search;
+// per-source launches cost their launch gaps and tails, and an earlier
+// one-launch form that looked the source up per element was slower still).
+constexpr int kImportMaxSrc = 64;  // II_MAX_PARTS
+constexpr uint32_t kImportPer = kBlock * 8;
+struct ImportSrc {
+    uint32_t n;
+    uint32_t bstart[kImportMaxSrc + 1];
+    const uint64_t* p[kImportMaxSrc];
+    uint64_t np[kImportMaxSrc], wbase[kImportMaxSrc], pbase[kImportMaxSrc];
+};
 template <bool k32>
-__global__ __launch_bounds__(kBlock) void k_import_pairs(const uint64_t* __restrict__ pairs, uint64_t np, uint64_t wbase,
-                                                         const uint64_t* __restrict__ wrec,
+__global__ __launch_bounds__(kBlock) void k_import_pairs(ImportSrc src, const uint64_t* __restrict__ wrec,
                                                          const uint32_t* __restrict__ remap, void* __restrict__ out,
                                                          int f32) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < np; i += (uint64_t)gridDim.x * kBlock) {
-        uint64_t r = pairs[i];
-        uint64_t slot = wrec[wbase + (r >> 32)] >> 32;
-        if (k32) static_cast<uint32_t*>(out)[i] = (remap[slot] << f32) | (uint32_t)r;
-        else static_cast<uint64_t*>(out)[i] = ((uint64_t)remap[slot] << 32) | (r & 0xFFFFFFFFull);
+    const uint32_t b = blockIdx.x;
+    if (b >= src.bstart[src.n]) return;
+    uint32_t lo = 0, hi = src.n - 1;  // the last source whose first workgroup is <= b
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (src.bstart[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const uint32_t s = __builtin_amdgcn_readfirstlane(lo);
+    const uint64_t* __restrict__ pairs = src.p[s];
+    const uint64_t np = src.np[s], wbase = src.wbase[s], pbase = src.pbase[s];
+    const uint64_t i0 = (uint64_t)(b - src.bstart[s]) * kImportPer;
+    const uint64_t i1 = i0 + kImportPer < np ? i0 + kImportPer : np;
+    // three rounds of loads in flight (pairs, word records, remap), not one chain per pair
+    constexpr int kQ = kImportPer / kBlock;
+    uint64_t r[kQ], slot[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock + threadIdx.x;
+        r[q] = i < i1 ? pairs[i] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock + threadIdx.x;
+        slot[q] = i < i1 ? wrec[wbase + (r[q] >> 32)] >> 32 : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock + threadIdx.x;
+        if (i < i1) {
+            const uint32_t lex = remap[slot[q]];
+            if (k32) static_cast<uint32_t*>(out)[pbase + i] = (lex << f32) | (uint32_t)r[q];
+            else static_cast<uint64_t*>(out)[pbase + i] = ((uint64_t)lex << 32) | (r[q] & 0xFFFFFFFFull);
+        }
     }
 }
 // The packed layout's geometry for ONE bucket of n u32 records from index 0
@@ -2415,7 +2454,9 @@ __device__ __forceinline__ uint64_t merge_corank(const K* __restrict__ A, uint64
     return lo;
 }
 
-// split[tile] = A-elements before the tile's first output, one thread per tile boundary
+// split[tile] = A-elements before the tile's first output, one thread per tile
+// boundary (a wave per boundary searching 64 points per round trip measured
+// slower: owner sort 0.70 -> 0.99 ms, 64 scattered loads per lane group per step)
 template <class K>
 __global__ __launch_bounds__(kBlock) void k_merge_partition(const K* __restrict__ src, MergeRound mr,
                                                             uint64_t* __restrict__ split) {

@@ -20,7 +20,7 @@ import os
 import subprocess
 import sys
 
-KERNELS = "k_tok_emit|k_tok_count|k_tok_resolve|k_long_verify|k_sort0_compact|k_radix_scatter|k_onesweep|k_seg_hist|k_radix_hist|k_uniq|k_fmt_posts"
+KERNELS = "k_tok_emit|k_tok_count|k_tok_resolve|k_long_verify|k_sort0_compact|k_radix_scatter|k_msd_scatter|k_onesweep|k_seg_hist|k_radix_hist|k_uniq|k_fmt_posts"
 
 
 def run(out, bench_args):
