@@ -262,6 +262,11 @@ static int run_scan(ii_ctx* c, Op op, uint64_t n, uint64_t* d_total) {
         if (d_total) HIPCK(hipMemsetAsync(d_total, 0, sizeof(uint64_t), c->st));
         return II_OK;
     }
+    if (n <= kScanSingleMax) {  // (one launch)
+        k_scan_single<Op><<<1, kScanSingleThreads, 0, c->st>>>(op, n, d_total);
+        HIPCK(hipGetLastError());
+        return II_OK;
+    }
     uint64_t nch = std::min<uint64_t>(kMaxChunks, (n + kBlock - 1) / kBlock);
     uint64_t chunk = ((n + nch - 1) / nch + kBlock - 1) / kBlock * kBlock;
     nch = (n + chunk - 1) / chunk;

@@ -165,6 +165,49 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(Op op, uint64_t n, uint64
     }
 }
 
+// Small scans in ONE launch (n <= kScanSingleMax): one 1024-thread workgroup,
+// 16 consecutive items per thread per round, a running base across rounds;
+// *total = the sum.  The three-launch form costs ~20 us of launches and gaps
+// whatever n is, which the radix passes over a few 10^5 dictionary keys (one
+// table scan each) paid eight times per dictionary.
+constexpr int kScanSingleThreads = 1024, kScanSingleItems = 16;
+constexpr uint64_t kScanSingleMax = 2ull * kScanSingleThreads * kScanSingleItems;
+template <class Op>
+__global__ __launch_bounds__(kScanSingleThreads) void k_scan_single(Op op, uint64_t n, uint64_t* total) {
+    constexpr int NW = kScanSingleThreads / 64;
+    __shared__ uint64_t lds[NW];
+    uint64_t run = 0;
+    for (uint64_t base = 0; base < n; base += (uint64_t)kScanSingleThreads * kScanSingleItems) {
+        const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanSingleItems;
+        uint64_t v[kScanSingleItems];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kScanSingleItems; j++) {
+            v[j] = i0 + j < n ? op.value(i0 + j) : 0;
+            sum += v[j];
+        }
+        const uint64_t inc = wave_incl_scan(sum);
+        if (lane_id() == 63) lds[wave_id()] = inc;
+        __syncthreads();
+        uint64_t wb = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint64_t x = lds[w];
+            if (w < wave_id()) wb += x;
+            tot += x;
+        }
+        __syncthreads();
+        uint64_t ex = run + wb + inc - sum;
+#pragma unroll
+        for (int j = 0; j < kScanSingleItems; j++) {
+            if (i0 + j < n) op.emit(i0 + j, ex, v[j]);
+            ex += v[j];
+        }
+        run += tot;
+    }
+    if (threadIdx.x == 0 && total) *total = run;
+}
+
 // ----------------------------------------------------------------------------
 // Stable LSD radix sort, 8-bit digits.  Keys u64 (digit taken from bits
 // [shift, shift+8)), optional u32 payload.  Each pass: histogram per chunk
