@@ -929,6 +929,9 @@ __global__ __launch_bounds__(NT) void k_seg_hist(const uint32_t* __restrict__ re
 // records [btile[h] * tile, + count of h) are valid; the look-back stops at
 // the bucket's first tile, which publishes an inclusive prefix at once.
 // Digit d of bucket h starts at the bucket's padded start + dbase[h * dstride + d].
+// (kLbPer: look-back granules per lane, 8 tiles per round trip per digit; 1 or
+// 4 measured no faster in round 4, at config3 or on the rank-7 share whose
+// buckets span ~190 tiles.)
 // (launch bound of 6 waves per SIMD: without one the compiler spent 256 VGPRs
 // with spills, one workgroup per CU, 2.4x slower than k_onesweep.  Round 4,
 // dropped: a workgroup claiming two tiles and loading both up front — its
