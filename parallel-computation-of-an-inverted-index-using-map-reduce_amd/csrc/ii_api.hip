@@ -73,7 +73,7 @@ struct ii_ctx {
     DBuf tied, tpos, rid, rfirst, tdict, tk, tk2, tv, tv2;
     // reduce / order / format
     DBuf uniq, pstart, pstop, pstart_w, pstop_w, okey, okey2, oval, oval2, P, loff, out, letter_off;
-    DBuf uniq_x, pstart_x;  // exchange after a word-id reduce: the pairs in lexid order (letter_points)
+    DBuf pstart_x;  // exchange after a word-id reduce: each word's first pair in lexid order (letter_points)
     DBuf mstart, mend;      // ii_import merge: per (word, source) run start / end -> merged offset
     DBuf moff;              // ii_import merge-path rounds: the left run's share before every tile (k_merge_partition)
     DBuf wmap, lexw, widl;  // wid keys (single-GPU reduce): big slot -> wid, wid -> lexid, lexid -> wid
@@ -86,7 +86,7 @@ struct ii_ctx {
     uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
     uint64_t lb_epoch = 0;       // epoch of the last onesweep pass
     bool wid_pairs = false; // the partial index came from a wid-keyed sort (no letter-contiguous pairs)
-    bool xpairs = false;    // uniq_x / pstart_x hold this partial index's pairs in lexid order
+    bool xpairs = false;    // pstart_x holds this partial index's lexid-order word starts
     uint64_t NW = 0;        // wid range
     // partial-file emitter (ii_partials)
     DBuf ppieces, pcnt, pout, ploff;
@@ -789,7 +789,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->woff,     &c->pts,    &c->pend,  &c->pend_cnt, &c->kept,
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
-                   &c->dhist,    &c->lbstat, &c->ticket, &c->uniq_x, &c->pstart_x, &c->msd, &c->tbk, &c->moff,
+                   &c->dhist,    &c->lbstat, &c->ticket, &c->pstart_x, &c->msd, &c->tbk, &c->moff,
                    &c->partial2, &c->rtable2, &c->kept2, &c->drank, &c->g64};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
@@ -1629,9 +1629,9 @@ extern "C" int ii_reduce(ii_ctx* c, int copy_text) {
 
 // ----------------------------------------------------------------- exchange
 // Per-letter points of the partial index (first word / pair / arena byte).
-// After a word-id reduce the exported pairs come from a lexid-ordered copy
-// (uniq_x / pstart_x, k_pairs_by_lexid), made once per reduce.
-static const uint64_t* export_pairs(ii_ctx* c) { return P_<uint64_t>(c->wid_pairs ? c->uniq_x : c->uniq); }
+// After a word-id reduce the words' lexid-order pair starts (pstart_x) are
+// scanned once per reduce; ii_export places the pairs by them.
+// (a word-id reduce's pairs are exported from their word-id order by k_export_pairs_wid)
 static int letter_points(ii_ctx* c) {
     const uint64_t V = c->V;
     if (V == 0 || c->T == 0) {
@@ -1639,16 +1639,11 @@ static int letter_points(ii_ctx* c) {
         return II_OK;
     }
     const uint64_t* ps = P_<uint64_t>(c->pstart);
-    if (c->wid_pairs) {
+    if (c->wid_pairs) {  // the pairs' lexid-order starts (the export places each pair by them)
         CK(grow(c->pstart_x, sizeof(uint64_t) * (V + 1)));
-        CK(grow(c->uniq_x, sizeof(uint64_t) * std::max<uint64_t>(c->U, 1)));
         uint64_t* psx = P_<uint64_t>(c->pstart_x);
         if (!c->xpairs) {
             CK(run_scan(c, OpRunLen{ps, P_<uint64_t>(c->pstop), psx}, V, psx + V));
-            if (c->U)
-                k_pairs_by_lexid<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(
-                    P_<uint64_t>(c->uniq), c->U, P_<uint32_t>(c->lexw), ps, psx, P_<uint64_t>(c->uniq_x));
-            HIPCK(hipGetLastError());
             c->xpairs = true;
         }
         ps = psx;
@@ -1724,6 +1719,10 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
     if (c->planned_parts != nparts) return II_ERR_STATE;
     LIVE_OR_FAIL();
     HIPCK(hipSetDevice(c->dev));
+    static_assert(kExportMaxParts >= II_MAX_PARTS, "one export launch for every part");
+    ExportParts xp;
+    memset(&xp, 0, sizeof(xp));
+    xp.n = (uint32_t)nparts;
     for (int r = 0; r < nparts; r++) {
         if (send_off[r] & 7) return II_ERR_ARG;
         const int lo = c->part_lo[r], hi = c->part_hi[r];
@@ -1735,15 +1734,24 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
         uint8_t* arena = seg + 64 + 8 * np;
         const uint64_t id_lo1 = c->h_fid.empty() ? 0 : 1ull + c->h_fid.front();
         const uint64_t id_hi1 = c->h_fid.empty() ? 0 : 1ull + c->h_fid.back();
+        xp.j0[r] = (uint32_t)a[0];
+        xp.j0[r + 1] = (uint32_t)b[0];
+        xp.p0[r] = a[1];
+        xp.dst[r] = pairs;
         k_export_header<<<1, 64, 0, c->st>>>((uint64_t*)seg, nw, np, ab, lo, hi, id_lo1, id_hi1);
-        if (np)
+        if (np && !c->wid_pairs)
             k_export_pairs<<<(uint32_t)std::min<uint64_t>(8192, grid_for(np)), kBlock, 0, c->st>>>(
-                export_pairs(c), a[1], b[1], (uint32_t)a[0], pairs);
+                P_<uint64_t>(c->uniq), a[1], b[1], (uint32_t)a[0], pairs);
         if (nw)
             k_export_words<<<grid_for(nw), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey),
                                                               P_<uint64_t>(c->lrep), P_<uint32_t>(c->llen),
                                                               P_<uint64_t>(c->woff), (uint32_t)a[0], (uint32_t)b[0],
                                                               arena);
+        HIPCK(hipGetLastError());
+    }
+    if (c->wid_pairs && c->U) {  // every part's pairs in one pass over the word-id order
+        k_export_pairs_wid<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(
+            P_<uint64_t>(c->uniq), c->U, P_<uint32_t>(c->lexw), P_<uint64_t>(c->pstart), P_<uint64_t>(c->pstart_x), xp);
         HIPCK(hipGetLastError());
     }
     HIPCK(hipStreamSynchronize(c->st));

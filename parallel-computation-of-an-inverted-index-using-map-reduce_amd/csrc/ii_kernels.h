@@ -2238,12 +2238,11 @@ struct OpWordArena {
     __device__ void emit(uint64_t j, uint64_t ex, uint64_t) const { woff[j] = ex; }
 };
 
-// Exchange after a word-id reduce: the pairs re-laid out in lexicographic
-// word order (the order export segments carry), keyed by lexid: pair s
-// (grouped by word id) of word j = lexw[wid] goes to psx[j] + (s - ps[j]),
-// psx = exclusive scan of the words' pair counts in lexid order.  One read
-// and one write per pair instead of sorting the tokens by lexid (whose first
-// pass gathers a map entry for every word).
+// Exchange after a word-id reduce: in lexicographic word order (the order
+// export segments carry) pair s (grouped by word id) of word j = lexw[wid] is
+// the (psx[j] + s - ps[j])-th, psx = exclusive scan of the words' pair counts
+// in lexid order (k_export_pairs_wid) — instead of sorting the tokens by lexid
+// (whose first pass gathers a map entry for every word).
 struct OpRunLen {
     const uint64_t* ps;
     const uint64_t* pe;
@@ -2251,16 +2250,6 @@ struct OpRunLen {
     __device__ uint64_t value(uint64_t j) const { return pe[j] - ps[j]; }
     __device__ void emit(uint64_t j, uint64_t ex, uint64_t) const { psx[j] = ex; }
 };
-__global__ __launch_bounds__(kBlock) void k_pairs_by_lexid(const uint64_t* __restrict__ uniq, uint64_t U,
-                                                           const uint32_t* __restrict__ lexw,
-                                                           const uint64_t* __restrict__ ps,
-                                                           const uint64_t* __restrict__ psx, uint64_t* __restrict__ out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < U; i += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t r = uniq[i];
-        const uint32_t j = lexw[r >> 32];
-        out[psx[j] + (i - ps[j])] = ((uint64_t)j << 32) | (r & 0xFFFFFFFFull);
-    }
-}
 
 // per letter l: first word, first pair, first arena byte
 __global__ void k_letter_points(const uint32_t* __restrict__ letter_start, const uint64_t* __restrict__ post_start,
@@ -2285,6 +2274,47 @@ __global__ __launch_bounds__(kBlock) void k_export_words(const uint8_t* __restri
     uint32_t len = lex_len[j];
     write_word(text, nbytes, lex_key[j], lex_rep[j], len, o);
     o[len] = ' ';
+}
+
+// Export of a word-id reduce's pairs straight from their word-id order (no
+// lexid-ordered copy first): pair i of word w (lexid j = lexw[w]) is the
+// (psx[j] + i - ps[j])-th pair in lexid order; the part whose lexid range
+// holds j (parts in LDS, a binary search over <= II_MAX_PARTS starts) gets it
+// as (j - j0) << 32 | id0 at dst + that index - the part's first pair.  (The
+// copy, k_pairs_by_lexid, wrote and re-read 16 bytes a pair more.)
+constexpr int kExportMaxParts = 64;  // II_MAX_PARTS
+struct ExportParts {
+    uint32_t n;
+    uint32_t j0[kExportMaxParts + 1];  // first lexid of part r (j0[n] = V)
+    uint64_t p0[kExportMaxParts];      // its first pair in lexid order
+    uint64_t* dst[kExportMaxParts];    // its segment's pair array
+};
+__global__ __launch_bounds__(kBlock) void k_export_pairs_wid(const uint64_t* __restrict__ uniq, uint64_t U,
+                                                             const uint32_t* __restrict__ lexw,
+                                                             const uint64_t* __restrict__ ps,
+                                                             const uint64_t* __restrict__ psx, ExportParts parts) {
+    __shared__ uint32_t s_j0[kExportMaxParts + 1];
+    __shared__ uint64_t s_p0[kExportMaxParts];
+    __shared__ uint64_t* s_dst[kExportMaxParts];
+    for (uint32_t r = threadIdx.x; r <= parts.n; r += kBlock) {
+        s_j0[r] = parts.j0[r];
+        if (r < parts.n) {
+            s_p0[r] = parts.p0[r];
+            s_dst[r] = parts.dst[r];
+        }
+    }
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < U; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t rr = uniq[i];
+        const uint32_t j = lexw[rr >> 32];
+        uint32_t lo = 0, hi = parts.n - 1;  // the last part with j0 <= j
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (s_j0[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        s_dst[lo][psx[j] + (i - ps[j]) - s_p0[lo]] = ((uint64_t)(j - s_j0[lo]) << 32) | (rr & 0xFFFFFFFFull);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_export_pairs(const uint64_t* __restrict__ uniq, uint64_t p0, uint64_t p1,
