@@ -588,7 +588,9 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
     uint32_t* out32 = reinterpret_cast<uint32_t*>(*k);
     constexpr int NTs = kScatterThreads, ITs = kScatterItems;
-    if (wide) {  // (for 8-bit top digits k_msd_scatter<.., 256> measured 0.1 ms slower than k_radix_scatter<kPack>)
+    // (for 8-bit top digits k_msd_scatter<.., 256> measured 0.1 ms slower than k_radix_scatter<kPack>, also
+    // with 8- or 12-record tiles at 6 waves per SIMD, 3 workgroups per CU)
+    if (wide) {
         auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
                           : k_msd_scatter<NTs, ITs, kMsdMax>;
         wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
