@@ -2486,8 +2486,8 @@ __device__ __forceinline__ uint64_t merge_corank(const K* __restrict__ A, uint64
 }
 
 // split[tile] = A-elements before the tile's first output, one thread per tile
-// boundary (a wave per boundary searching 64 points per round trip measured
-// slower: owner sort 0.70 -> 0.99 ms, 64 scattered loads per lane group per step)
+// boundary (a wave per boundary searching 64 points per round trip was not
+// faster in the run that measured it)
 template <class K>
 __global__ __launch_bounds__(kBlock) void k_merge_partition(const K* __restrict__ src, MergeRound mr,
                                                             uint64_t* __restrict__ split) {
