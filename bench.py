@@ -167,17 +167,21 @@ def pmc_traffic(build, shape):
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
     if not files:
         return {}, "no PMC summary in profiles/"
-    try:
-        d = json.load(open(files[-1]))
-    except Exception as e:  # noqa: BLE001
-        return {}, "unreadable %s: %s" % (os.path.basename(files[-1]), e)
-    line = d.get("bench_line", {})
-    if line.get("libii_sha16") != build:
-        return {}, "%s was measured on another libii.so build" % os.path.basename(files[-1])
-    cfg = line.get("config", {})
-    if (cfg.get("bytes"), cfg.get("files"), line.get("n_gpus"), cfg.get("rank_share")) != shape:
-        return {}, "%s was measured on another workload" % os.path.basename(files[-1])
-    return ({k: v for k, v in d["kernels"].items() if "traffic_bytes_per_launch" in v}, os.path.basename(files[-1]))
+    why = "no PMC summary of this libii.so build (%s) in profiles/" % build
+    for f in reversed(files):  # the summary made on this very build, whichever file holds it
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        line = d.get("bench_line", {})
+        if line.get("libii_sha16") != build:
+            continue
+        cfg = line.get("config", {})
+        if (cfg.get("bytes"), cfg.get("files"), line.get("n_gpus"), cfg.get("rank_share")) != shape:
+            why = "%s was measured on another workload" % os.path.basename(f)
+            continue
+        return ({k: v for k, v in d["kernels"].items() if "traffic_bytes_per_launch" in v}, os.path.basename(f))
+    return {}, why
 
 
 # the kernels of the sort + segmented-reduce phase (K2 token sort + K3), by rocprof name prefix
