@@ -913,6 +913,13 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
     const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1];
     const bool fsame = f_lo == f_hi;
     const bool narrow = chunk_narrow(cap, cf, c);
+    // a chunk over a few files (configs[4]'s small-file shares): the starts of its files after the first,
+    // wave-uniform, so that a token's file is a few compares instead of a dependent load per batch
+    constexpr uint32_t kFb = 3;
+    const bool fsmall = f_hi - f_lo <= kFb;
+    uint64_t fb[kFb];
+#pragma unroll
+    for (uint32_t k = 0; k < kFb; k++) fb[k] = !fsame && f_lo + 1 + k <= f_hi ? file_start[f_lo + 1 + k] : ~0ull;
     const uint64_t cbase = chunk_base(chunk_off, cap, c);
     uint32_t* const rec32 = reinterpret_cast<uint32_t*>(rec + cbase);
     const uint32_t rot = rec_rot(cap, c), wrap = rec_wrap(cap);
@@ -999,7 +1006,13 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
                 if (narrow) {
                     rec32[jr] = slot;
                 } else {
-                    const uint32_t f = fsame ? f_lo : file_of(file_start, f_lo, f_hi, lo + p);
+                    uint32_t f = f_lo;
+                    if (fsmall) {
+#pragma unroll
+                        for (uint32_t k = 0; k < kFb; k++) f += lo + p >= fb[k];
+                    } else {
+                        f = file_of(file_start, f_lo, f_hi, lo + p);
+                    }
                     rec[cbase + jr] = ((uint64_t)slot << 32) | f;
                 }
             } else if (pf) {
