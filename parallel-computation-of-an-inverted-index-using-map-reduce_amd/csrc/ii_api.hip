@@ -698,14 +698,14 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         const uint32_t* btile = g.btile;
         const uint64_t ntiles = 2ull * c->pk_ntb;  // at most: the spare ones leave at once
         CK(lookback_pass(c, 2 * ntiles));
-        k_uniq_sweep<true><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
+        (fmap ? k_uniq_sweep<true, true> : k_uniq_sweep<true, false>)<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             nullptr, n, reinterpret_cast<const uint32_t*>(r), c->pk_ncap, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
             P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64, c->dth);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
-        k_uniq_sweep<false><<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
+        (fmap ? k_uniq_sweep<false, true> : k_uniq_sweep<false, false>)<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
             P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW,
             fmap, u32, g64, c->dth);

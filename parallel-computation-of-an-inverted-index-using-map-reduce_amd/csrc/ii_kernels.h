@@ -1675,8 +1675,8 @@ static_assert(kUniqItems == 4, "per-item prefixes travel as 8-bit (flags) and 16
 
 // id0 of a record's file: the records of a map carry shard-local file indices
 // (k_chunk_files); fmap = the mapped files' id0s, or null when index == id0
-// (the file table is 0, 1, 2, ...; the owners' merged pairs carry id0s)
-__device__ __forceinline__ uint32_t file_id0(const uint32_t* __restrict__ fmap, uint32_t f) { return fmap ? fmap[f] : f; }
+// (the file table is 0, 1, 2, ...; the owners' merged pairs carry id0s).
+// K3 (k_uniq_sweep<kPacked, kFmap>) gathers fmap[f] only in its kFmap instance.
 
 // digits of v = id0 + 1 <= 2^32 (1..10), branch-free
 __device__ __forceinline__ uint32_t id_digits(uint64_t v) {
@@ -1764,7 +1764,12 @@ constexpr int kUniqSweepTile = kUniqSub * kUniqTile;  // 4096 records
 // bucket's).  The last record of each bucket closes its word (post_end),
 // which the dense form leaves to the next word's start and k_post_last.
 static_assert(kSweepTile == 2 * kUniqSweepTile, "K3 tile = half a packed-sort tile");
-template <bool kPacked>
+// kFmap: the records carry shard-local file indices (fmap != null; the
+// launcher picks kFmap = false only for fmap == null, index == id0): their id0s
+// are gathered for all sub-tiles at once, before the look-back (the gathers
+// miss L1 for a share of 4·10^5 files and were one dependent round trip per
+// sub-tile in the write phase).
+template <bool kPacked, bool kFmap = false>
 __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const uint64_t* __restrict__ rec, uint64_t n,
                                                        const uint32_t* __restrict__ rec32, uint64_t ncap,
                                                        const uint32_t* __restrict__ btile,
@@ -1872,7 +1877,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
                 c8 |= 1u << (8 * q);
-                const uint32_t d = pair_bytes(fmap, dth, (uint32_t)r);
+                const uint32_t d = pair_bytes(kFmap ? fmap : nullptr, dth, (uint32_t)r);
                 if (q < 2) bl += d << (16 * q);
                 else bh += d << (16 * (q - 2));
                 tcount++;
@@ -1926,6 +1931,20 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
         if (t == 0) {
             s_tot[k][0] = tc;
             s_tot[k][1] = tb;
+        }
+    }
+    uint32_t gid[kUniqSub * kUniqItems];  // kFmap: every flagged item's id0 (in flight during the look-back)
+#pragma unroll
+    for (int k = 0; k < kUniqSub; k++) {
+        const uint64_t ec = k == 0 ? exc0 : k == 1 ? exc1 : k == 2 ? exc2 : exc3;
+#pragma unroll
+        for (int q = 0; q < kUniqItems; q++) {
+            gid[k * kUniqItems + q] = 0u;
+            if (kFmap && ((ec >> (16 * q)) & 0x8000ull)) {
+                uint64_t r, pv;
+                item(k, q, r, pv);
+                gid[k * kUniqItems + q] = fmap[(uint32_t)r];
+            }
         }
     }
     // look-back, wave 0: lanes 0..31 walk the pair counts, lanes 32..63 the
@@ -1991,11 +2010,14 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                 const uint64_t uu = rc + (f & 0x7FFFull);
                 const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
                 const bool wstart = pv == ~0ull || key != pkey;
+                const uint32_t id0 = !kFmap ? (uint32_t)r
+                                   : k == 0 ? gid[q] : k == 1 ? gid[kUniqItems + q]
+                                   : k == 2 ? gid[2 * kUniqItems + q] : gid[3 * kUniqItems + q];
                 if (uniq32) {  // (uniform)
-                    uniq32[uu] = file_id0(fmap, (uint32_t)r) | (wstart ? kPairFirst : 0u);
+                    uniq32[uu] = id0 | (wstart ? kPairFirst : 0u);
                     if ((uu & 63u) == 0) g64[uu >> 6] = key;
                 } else {
-                    uniq[uu] = (r & ~0xFFFFFFFFull) | file_id0(fmap, (uint32_t)r);
+                    uniq[uu] = (r & ~0xFFFFFFFFull) | id0;
                 }
                 // P is read at word starts (k_fmt_words, OpLineOff) and at the
                 // first posting of every 64 (k_fmt_posts) only
