@@ -341,16 +341,23 @@ static int s0_geometry(ii_ctx* c, S0Geom* g) {
     g->ncol = (nch_in + g->group - 1) / g->group;
     return II_OK;
 }
-template <bool kWid, bool kWideD>
+template <bool kWid, bool kWideD, bool kHashD = false>
 static void sort0_inst(ii_ctx* c, const S0Geom& g, const uint64_t* k, uint64_t* k2, int shift, uint32_t dmask,
                        uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2, uint64_t* dhist) {
-    k_sort0_compact<kWid, kWideD><<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
+    k_sort0_compact<kWid, kWideD, kHashD><<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
         k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
         (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files));
 }
 static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k, uint64_t* k2, int shift,
                          uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
-                         uint64_t* dhist, bool wide = false) {
+                         uint64_t* dhist, bool wide = false, bool hashd = false) {
+    if (hashd) {  // (the packed sort only: no later-digit counts)
+        if (wid && wide) sort0_inst<true, true, true>(c, g, k, k2, shift, dmask, table, remap, kept, 0, 0, nullptr);
+        else if (wid) sort0_inst<true, false, true>(c, g, k, k2, shift, dmask, table, remap, kept, 0, 0, nullptr);
+        else if (wide) sort0_inst<false, true, true>(c, g, k, k2, shift, dmask, table, remap, kept, 0, 0, nullptr);
+        else sort0_inst<false, false, true>(c, g, k, k2, shift, dmask, table, remap, kept, 0, 0, nullptr);
+        return;
+    }
     if (wid && wide) sort0_inst<true, true>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
     else if (wid) sort0_inst<true, false>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
     else if (wide) sort0_inst<false, true>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
@@ -522,6 +529,19 @@ static int packed_top_bits(int W, int F) {
     return (m <= kMsdMaxBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
 }
 
+// The first pass's dedup for the packed sort: the record set (kHashD) when the
+// files average fewer than kHashDedupTokens tokens (configs[4]'s small-file
+// shares: 3.9·10^3), the epoch bitmap otherwise (config3: 1.4·10^5 per file,
+// more distinct pairs per file than the set holds).  II_S0_DEDUP=set|bitmap
+// (test and A/B knob) forces one.
+constexpr uint64_t kHashDedupTokens = 16384;
+static bool dedup_by_set(const ii_ctx* c, uint64_t n) {
+    const char* e = getenv("II_S0_DEDUP");
+    if (e && !strcmp(e, "set")) return true;
+    if (e && !strcmp(e, "bitmap")) return false;
+    return c->nfiles && n < kHashDedupTokens * (uint64_t)c->nfiles;
+}
+
 // The packed sort's bucket geometry and LSD digit counts in c->msd (sized for
 // kMsdMax buckets): bstart[kMsdMax + 1] | pad[kMsdMax] | btile (u32)[kMsdMax + 1]
 // | gh[2 kMsdMax kRadix] | gbase[2 kMsdMax kRadix]
@@ -576,7 +596,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     const uint32_t dmask = nb - 1u;
 
     HIPCK(hipEventRecord(c->ev_c0[0], c->st));
-    launch_sort0(c, s0, wid, *k, *k2, shift, dmask, table, remap0, kept, 0, 0, nullptr, wide);
+    launch_sort0(c, s0, wid, *k, *k2, shift, dmask, table, remap0, kept, 0, 0, nullptr, wide, dedup_by_set(c, n));
     HIPCK(hipEventRecord(c->ev_c0[1], c->st));
     CK(run_scan(c, OpInPlace{table}, (uint64_t)rows * nch, totals + 4));
     k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);

@@ -1490,7 +1490,26 @@ constexpr int kLaterDigits = 2;                 // digits counted for the oneswe
 // kWideD: top digits of up to kMsdMaxBits bits (the packed sort's wide MSD
 // split, k_msd_scatter): one count row of kMsdMax digits shared by the waves
 // (16 per-wave rows would not fit beside the bitmap); rows d <= dmask.
-template <bool kWid, bool kWideD = false>
+// kHashD (small files: a file's records span fewer than two tiles, so the
+// epoch bitmap deduplicated only the records of one file per tile and was
+// cleared on nearly every tile): the same 128 KiB hold an open-addressed set
+// of kHsSlots u32 entries (file mod 128) << 25 | slot, any slot below 2^25 - 1,
+// not only hot ones.  The set is cleared when the epoch has moved 64 files
+// past the last clear (ec), so every entry's file lies in [ec, ec + 128) and
+// its 7 bits name it; an entry whose file is below the tile's epoch belongs to
+// a finished file (files ascend through a range) and is taken over by the next
+// record that probes it.  Records outside [epoch, epoch + 64) or with larger
+// slots are kept unprobed.  A record is dropped only when its own entry is
+// found, i.e. a copy was inserted, and so kept; a full probe sequence keeps the
+// record (K3 drops what the first pass keeps twice).  (u64 entries of whole
+// records, half as many: 14.1 ms against the bitmap's 8.3 on configs[4]'s
+// rank-7 share, most first probes meeting a live entry.)
+constexpr uint32_t kHsSlots = kDedupWords;  // u32 entries in the bitmap's LDS
+constexpr int kHsProbe = 8;
+constexpr uint32_t kHsEmpty = ~0u;
+constexpr uint32_t kHsSlotLimit = (1u << 25) - 1u;  // slots below it are probed
+constexpr uint32_t kHsFileWin = 64;                 // files past the epoch that are probed
+template <bool kWid, bool kWideD = false, bool kHashD = false>
 __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
                                                            const uint64_t* __restrict__ voff, uint32_t nch_in,
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
@@ -1505,7 +1524,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     constexpr int kCntRows = kWideD ? 1 : NWv;
     constexpr int kCntD = kWideD ? kMsdMax : kRadix;
     __shared__ uint32_t cnt[kCntRows][kCntD];
-    __shared__ uint32_t bm[kBmWords];
+    __shared__ uint32_t bm[kBmWords];  // the bitmap, or (kHashD) the set
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
     __shared__ uint32_t s_cfid[kCMaxGroup];      // narrow chunk: its file id; ~0: u64 records
     __shared__ uint32_t s_later[kLaterDigits][kRadix];
@@ -1515,7 +1534,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     const uint32_t c0 = blockIdx.x * group, ng = c0 + group < nch_in ? group : nch_in - c0;
     for (int i = threadIdx.x; i < kCntRows * kCntD; i += NT) (&cnt[0][0])[i] = 0;
     for (int i = threadIdx.x; i < kLaterDigits * kRadix; i += NT) (&s_later[0][0])[i] = 0;
-    for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = 0;
+    for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = kHashD ? kHsEmpty : 0u;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
     for (uint32_t i = threadIdx.x; i <= ng; i += NT) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
     for (uint32_t i = threadIdx.x; i < ng; i += NT) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
@@ -1571,6 +1590,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     // the first tile's epoch: the file of the range's first record (every lane loads it)
     uint32_t epoch = lo >= hi ? 0u : s_cfid[0] != ~0u ? s_cfid[0] : (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo];
     uint32_t par = 0;
+    uint32_t ec = epoch;  // kHashD: the epoch of the set's last clear
     for (uint64_t tb = lo; tb < hi; tb += kTile, par ^= 1u) {
         uint64_t raw[kS0Items];
 #pragma unroll
@@ -1578,8 +1598,75 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             raw[k] = nfid[k] == ~0u ? nraw[k] : ((nraw[k] >> (32 * ((nodd >> k) & 1u))) << 32) | nfid[k];
         if (tb != lo && s_last[par ^ 1u] != epoch) {  // (workgroup-uniform) a new file: clear the bitmap
             epoch = s_last[par ^ 1u];
-            for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = 0;
-            __syncthreads();
+            if (!kHashD || epoch - ec >= kHsFileWin) {  // (kHashD: every 64 files)
+                for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = kHashD ? kHsEmpty : 0u;
+                ec = epoch;
+                __syncthreads();
+            }
+        }
+        uint32_t hkeep = 0;  // kHashD: the items the set keeps
+        if (kHashD) {
+            // first probes of all items at once (one LDS round trip for the loads, one for the
+            // CASes); the rest of a probe sequence, per item, only where another record took the entry
+            // (the entry index is recomputed where it is used: holding it spilled)
+            auto hs_of = [](uint32_t q) { return (q * 0x9E3779B1u) >> (32 - 15); };
+            static_assert(kHsSlots == 1u << 15, "hs_of yields 15 bits");
+            // an entry is free, or a finished file's: its file (ec + its 7 bits mod 128) below the epoch
+            auto hs_free = [&](uint32_t x) { return x == kHsEmpty || ec + (((x >> 25) - ec) & 127u) < epoch; };
+            uint32_t q[kS0Items], live = 0, slow = 0;
+            uint32_t e[kS0Items];
+#pragma unroll
+            for (int k = 0; k < kS0Items; k++) {
+                const uint32_t f = (uint32_t)raw[k], sl = (uint32_t)(raw[k] >> 32);
+                q[k] = ((f & 127u) << 25) | sl;
+                e[k] = kHsEmpty;
+                if (tb + tofs + (uint64_t)k * 64 < hi) {
+                    if (sl < kHsSlotLimit && f - epoch < kHsFileWin) {
+                        live |= 1u << k;
+                        e[k] = __hip_atomic_load(&bm[hs_of(q[k])], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        hkeep |= 1u << k;  // not probed: kept
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kS0Items; k++) {
+                if (!((live >> k) & 1u) || e[k] == q[k]) continue;  // a copy was inserted (and kept)
+                if (hs_free(e[k])) {
+                    const uint32_t o = atomicCAS(&bm[hs_of(q[k])], e[k], q[k]);
+                    if (o == e[k]) hkeep |= 1u << k;      // inserted: keep
+                    else if (o != q[k]) slow |= 1u << k;  // another record took it: probe on
+                } else {
+                    slow |= 1u << k;
+                }
+            }
+            while (slow) {  // (one item at a time, selected without indexing the arrays)
+                const int k = __builtin_ctz(slow);
+                slow &= slow - 1u;
+                uint32_t qk = q[0];
+#pragma unroll
+                for (int j = 1; j < kS0Items; j++) qk = j == k ? q[j] : qk;
+                uint32_t hh = hs_of(qk);
+                bool keepk = true;  // a full probe sequence keeps the record
+                for (int p = 0; p < kHsProbe; p++) {
+                    const uint32_t x = __hip_atomic_load(&bm[hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (x == qk) {
+                        keepk = false;
+                        break;
+                    }
+                    if (hs_free(x)) {
+                        const uint32_t o = atomicCAS(&bm[hh], x, qk);
+                        if (o == x) break;
+                        if (o == qk) {
+                            keepk = false;
+                            break;
+                        }
+                        continue;  // taken meanwhile: look at it again
+                    }
+                    hh = (hh + 1) & (kHsSlots - 1);
+                }
+                hkeep |= (uint32_t)keepk << k;
+            }
         }
         uint32_t keep = 0, wcount = 0;
         uint32_t pos[kS0Items];
@@ -1587,7 +1674,9 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
         for (int k = 0; k < kS0Items; k++) {
             bool ok = tb + tofs + (uint64_t)k * 64 < hi;
             const uint64_t slot = raw[k] >> 32;
-            if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
+            if (kHashD) {
+                ok = ok && ((hkeep >> k) & 1u);
+            } else if (ok && slot < kHotSlots && (uint32_t)raw[k] == epoch) {
                 const uint32_t bit = 1u << (slot & 31);
                 ok = !(atomicOr(&bm[slot >> 5], bit) & bit);
             }

@@ -482,6 +482,44 @@ def test_wide_top_digit_vs_oracle(env):
             os.environ.pop(k, None)
 
 
+@pytest.mark.parametrize("env", [{}, {"II_PACKED_M": "10"}, {"II_SORT_KEYS": "lexid"}])
+def test_first_pass_record_set_vs_oracle(env):
+    """The first pass's record-set dedup (k_sort0_compact<.., kHashD>), the
+    form small-file shares take (configs[4]'s rank 7: 3.9·10^3 tokens per
+    file): 9000 files of ~3 KB against the oracle, the set chosen by itself
+    and forced (II_S0_DEDUP=set) on 40 files of 1 MB, where live pairs
+    outnumber the set's entries and full probe sequences keep records.  On
+    small files it must keep fewer records than the epoch bitmap."""
+    small = ii_ctypes.zipf_corpus(27_000_000, 9000, 1_000_000, 53, threads=8)
+    large = ii_ctypes.zipf_corpus(40_000_000, 40, 1_000_000, 59, threads=8)
+    try:
+        os.environ.update(env)
+        for (t, off), force in ((small, None), (small, "bitmap"), (large, "set")):
+            off = off.tolist()
+            ids = list(range(len(off) - 1))
+            exp = oracle_index(t, off, ids)
+            if force:
+                os.environ["II_S0_DEDUP"] = force
+            try:
+                with ii_ctypes.Index(0) as ix:
+                    ix.map_host(t, off, ids)
+                    ix.reduce()
+                    assert_same(ix.letters(), exp, "%s II_S0_DEDUP=%s" % (env, force))
+                    st = ix.stats()
+                    assert st.sort_packed == 1
+                    kept = st.sorted_records
+            finally:
+                os.environ.pop("II_S0_DEDUP", None)
+            if force is None:
+                kept_set, pairs = kept, st.pairs
+                assert kept_set <= 1.05 * pairs, (kept_set, pairs)
+            elif force == "bitmap":
+                assert kept_set < 0.9 * kept, (kept_set, kept)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+
+
 def test_global_ids_of_a_share_stay_packed():
     """A rank's ii_partition share (main.c:300-323): 2000 files whose global ids
     span [0, 10^6) — the shape of a configs[4] rank.  The records carry 11-bit
