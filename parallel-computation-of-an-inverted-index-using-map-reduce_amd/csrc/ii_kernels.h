@@ -1506,6 +1506,7 @@ constexpr int kLaterDigits = 2;                 // digits counted for the oneswe
 // rank-7 share, most first probes meeting a live entry.)
 constexpr uint32_t kHsSlots = kDedupWords;  // u32 entries in the bitmap's LDS
 constexpr int kHsProbe = 8;
+constexpr int kHsRounds = 2;  // probe rounds batched over a thread's items (the rest: one item at a time)
 constexpr uint32_t kHsEmpty = ~0u;
 constexpr uint32_t kHsSlotLimit = (1u << 25) - 1u;  // slots below it are probed
 constexpr uint32_t kHsFileWin = 64;                 // files past the epoch that are probed
@@ -1640,15 +1641,35 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                     slow |= 1u << k;
                 }
             }
-            while (slow) {  // (one item at a time, selected without indexing the arrays)
+            if (slow) {  // second round, batched like the first: the next entry of every item passed on
+                uint32_t s2 = 0;
+#pragma unroll
+                for (int k = 0; k < kS0Items; k++)
+                    if ((slow >> k) & 1u)
+                        e[k] = __hip_atomic_load(&bm[(hs_of(q[k]) + 1u) & (kHsSlots - 1)], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                for (int k = 0; k < kS0Items; k++) {
+                    if (!((slow >> k) & 1u) || e[k] == q[k]) continue;
+                    if (hs_free(e[k])) {
+                        const uint32_t o = atomicCAS(&bm[(hs_of(q[k]) + 1u) & (kHsSlots - 1)], e[k], q[k]);
+                        if (o == e[k]) hkeep |= 1u << k;
+                        else if (o != q[k]) s2 |= 1u << k;
+                    } else {
+                        s2 |= 1u << k;
+                    }
+                }
+                slow = s2;
+            }
+            while (slow) {  // (one item at a time from entry + kHsRounds, selected without indexing the arrays)
                 const int k = __builtin_ctz(slow);
                 slow &= slow - 1u;
                 uint32_t qk = q[0];
 #pragma unroll
                 for (int j = 1; j < kS0Items; j++) qk = j == k ? q[j] : qk;
-                uint32_t hh = hs_of(qk);
+                uint32_t hh = (hs_of(qk) + (uint32_t)kHsRounds) & (kHsSlots - 1);
                 bool keepk = true;  // a full probe sequence keeps the record
-                for (int p = 0; p < kHsProbe; p++) {
+                for (int p = kHsRounds; p < kHsProbe; p++) {
                     const uint32_t x = __hip_atomic_load(&bm[hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (x == qk) {
                         keepk = false;
