@@ -62,6 +62,7 @@ PKG = os.path.join(REPO, "parallel-computation-of-an-inverted-index-using-map-re
 sys.path.insert(0, os.path.join(PKG, "bindings"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+K1_TEXT_RAW_PER_BYTE = 0.595  # raw FETCH_SIZE bytes per text byte of K1b's streamed reads (r3 calibration)
 LETTERS = "abcdefghijklmnopqrstuvwxyz"
 
 WORKLOADS = {
@@ -641,9 +642,9 @@ def main():
         traffic, traffic_src = pmc_traffic(build, (a.bytes if strong else a.bytes * world, a.files, world,
                                                    "%d/%d" % a.share if a.share else None))
         # sort + segmented-reduce phase (K2 token sort + K3 unique), three byte counts:
-        #  impl (frac, the primary figure): the bytes this build's kernels must move —
-        #          the first pass reads T records (u32 / u64 as K1 wrote them, counted
-        #          as 8 B) and writes the T_k kept ones (st.sort0_bytes), the passes after it as the
+        #  impl:   the bytes this build's kernels must move —
+        #          the first pass reads T records (4 B from narrow chunks' u32 word slots,
+        #          8 B from the others) and writes the T_k kept ones (st.sort0_bytes), the passes after it as the
         #          library counts them (st.sort_bytes: the packed form's u32 bucket
         #          passes), K3 reads the sorted records once (u32 in the packed form)
         #          and writes the pairs, the posting offsets P (every word start and
@@ -653,7 +654,8 @@ def main():
         #          the packed passes for u64 records they do not move (secondary)
         #  pmc:    HBM bytes the counters saw for the phase's kernels (rocprofv3
         #          FETCH_SIZE x correction + WRITE_SIZE, profiles/*_pmc_traffic.json
-        #          of this very build), when there is such a summary
+        #          of this very build), when there is such a summary: then `frac` is
+        #          pmc_frac (SURVEY §8d defines achieved HBM by the counters), else impl
         T, Tk, U, V = st.tokens, st.sorted_records, st.pairs, st.words
         sp = max(1, st.sort_passes)
         survey_b = 8 * T + 8 * Tk + sp * 16 * Tk + 8 * Tk + 8 * U + 16 * V
@@ -664,6 +666,27 @@ def main():
         ph_ms = sum(phase_ms) / len(phase_ms)
         ph_gbs = impl_b / (ph_ms * 1e-3) / 1e9 if ph_ms > 0 else 0.0
         pmc_b = pmc_phase_bytes(traffic) if traffic else None
+        impl_frac = ph_gbs / HBM_PEAK_GBS
+        pmc_frac = pmc_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if pmc_b and ph_ms > 0 else None
+        # K1b: SURVEY §8d's tokenize model (B + 12 T, 12-B canonical records) beside the library's
+        # B + 8 T; PMC traffic split into the streamed text and the hot-table probe lines: the text is
+        # read with 16-B loads whose 128-B requests FETCH_SIZE tallies at 64 B (x2, MI355X_MICROARCH.md),
+        # the probes' 64-B requests are tallied at full size (no x2).  The text share of the raw
+        # FETCH_SIZE is calibrated on the probe-free K1b variant (tools/k1_ablate, round 3:
+        # TCC_EA0_RDREQ 9.3e6 128-B requests = 0.595 raw FETCH bytes per text byte, incl. halos and
+        # the K1c tail's re-reads; profiles/r3_k1_pmc_1GB.txt)
+        B_emit = st.bytes
+        k1_survey_b = B_emit + 12 * T
+        k1 = kernel_entry(traffic, "ii::k_tok_emit")
+        k1_split = None
+        if "read_raw_bytes_per_launch" in k1:
+            raw = k1["read_raw_bytes_per_launch"]
+            text_raw = min(raw, K1_TEXT_RAW_PER_BYTE * B_emit)
+            probe = raw - text_raw
+            wr = k1["write_bytes_per_launch"]
+            k1_split = {"traffic": round(2 * text_raw + probe + wr), "traffic_text": round(2 * text_raw),
+                        "traffic_probe": round(probe), "traffic_write": round(wr),
+                        "probe_bytes_per_text_byte": round(probe / B_emit, 3) if B_emit else None}
         cpu = None
         if a.cpu_baseline != "none" and world == 1:
             cpu = cpu_baseline(a, text, off)
@@ -704,30 +727,44 @@ def main():
                        "parallelism": "files by size over %d GPU(s) + letter-range all-to-allv" % world
                        if world > 1 else "one GPU",
                        "letter_split": a.letter_split if world > 1 or a.share else None},
-            # dominant kernel: the tokenizer (K1b); algorithmic bytes = B + 8*T per launch
+            # dominant kernel: the tokenizer (K1b); algorithmic bytes per launch = SURVEY §8d's
+            # B + 12*T (12-B canonical records; `frac`), and the library's B + 8*T beside it
             "roofline": {"bound": "hbm", "kernel": "k_tok_emit (K1b tokenizer)",
-                         "achieved": round(em_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(em_achieved / HBM_PEAK_GBS, 4),
-                         "traffic": round(kernel_entry(traffic, "ii::k_tok_emit")["traffic_bytes_per_launch"])
-                         if "traffic_bytes_per_launch" in kernel_entry(traffic, "ii::k_tok_emit") else None,
-                         "traffic_raw": round(kernel_entry(traffic, "ii::k_tok_emit")["traffic_raw_bytes_per_launch"])
-                         if "traffic_raw_bytes_per_launch" in kernel_entry(traffic, "ii::k_tok_emit") else None,
-                         "traffic_source": traffic_src,
-                         "bytes_per_launch": st.emit_bytes, "ms_per_launch": round(em_ms, 4)},
+                         "achieved": round(k1_survey_b / (em_ms * 1e-3) / 1e9, 1) if em_ms > 0 else 0.0,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(k1_survey_b / (em_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if em_ms > 0 else 0.0,
+                         "bytes_per_launch": k1_survey_b, "model": "SURVEY §8d: B + 12 T",
+                         "achieved_b8t": round(em_achieved, 1), "frac_b8t": round(em_achieved / HBM_PEAK_GBS, 4),
+                         "bytes_per_launch_b8t": st.emit_bytes,
+                         # calibrated PMC traffic: x2 on the streamed text only (see K1_TEXT_RAW_PER_BYTE)
+                         "traffic": k1_split["traffic"] if k1_split else None,
+                         "traffic_text": k1_split["traffic_text"] if k1_split else None,
+                         "traffic_probe": k1_split["traffic_probe"] if k1_split else None,
+                         "traffic_write": k1_split["traffic_write"] if k1_split else None,
+                         "probe_bytes_per_text_byte": k1_split["probe_bytes_per_text_byte"] if k1_split else None,
+                         "traffic_fetch_x2": round(k1["traffic_bytes_per_launch"]) if "traffic_bytes_per_launch" in k1
+                         else None,
+                         "traffic_raw": round(k1["traffic_raw_bytes_per_launch"]) if "traffic_raw_bytes_per_launch" in k1
+                         else None,
+                         "traffic_note": "FETCH_SIZE counts Infinity-Cache hits too (MI355X_MICROARCH.md): the 8 MB "
+                                         "hot table's probe lines are mostly served on-die, not by HBM",
+                         "traffic_source": traffic_src, "ms_per_launch": round(em_ms, 4)},
             "roofline_sort": {"bound": "hbm", "kernel": "k_radix_scatter (token sort passes)",
                               "achieved": round(sc_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(sc_achieved / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": st.scatter_bytes, "ms_per_launch": round(sc_ms, 4)},
             "roofline_sort_phase": {"bound": "hbm", "phase": "token sort + segmented unique (K2 + K3)",
-                                    "model": "bytes this build's kernels must move (impl)",
-                                    "achieved": round(ph_gbs, 1), "peak": HBM_PEAK_GBS,
-                                    "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 4),
+                                    "model": "PMC counters (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this build)"
+                                    if pmc_frac is not None else "bytes this build's kernels must move (impl)",
+                                    "achieved": round((pmc_frac if pmc_frac is not None else impl_frac) * HBM_PEAK_GBS, 1),
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(pmc_frac if pmc_frac is not None else impl_frac, 4),
+                                    "impl_frac": round(impl_frac, 4), "impl_achieved": round(ph_gbs, 1),
                                     "bytes_per_step": impl_b, "survey_bytes_per_step": survey_b,
                                     "survey_frac": round(survey_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                     if ph_ms > 0 else 0.0,
                                     "pmc_bytes_per_step": round(pmc_b) if pmc_b else None,
-                                    "pmc_frac": round(pmc_b / (ph_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                    if pmc_b and ph_ms > 0 else None,
+                                    "pmc_frac": round(pmc_frac, 4) if pmc_frac is not None else None,
                                     "ms_per_step": round(ph_ms, 4),
                                     "first_pass": {"kernel": "k_sort0_compact", "ms": round(st.sort0_ms, 4),
                                                    "bytes": st.sort0_bytes,

@@ -86,7 +86,8 @@ typedef struct {
     double resolve_ms;     /* k_long_verify, the exactness pass of hashed (> 12-letter) keys */
     uint64_t resolved_tokens; /* tokens K1b's fast path left to its K1c tail (general path, full hot bucket, raced claim) */
     double sort0_ms;       /* first token-sort pass: dedup + lexid remap + compaction (k_sort0_compact) */
-    uint64_t sort0_bytes;  /* its algorithmic bytes: 8 B per record read + 8 B per kept record written */
+    uint64_t sort0_bytes;  /* its algorithmic bytes: the records read (4 B each from narrow chunks, whose u32
+                              word slots K1b wrote, 8 B from the others) + 8 B per kept record written */
     /* ii_map_files only (0 otherwise): host wall time of reading the files and
      * uploading them (pipelined pread -> pinned windows -> async H2D), and
      * the bytes uploaded */

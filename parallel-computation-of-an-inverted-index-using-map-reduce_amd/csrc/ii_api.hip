@@ -341,12 +341,20 @@ static int s0_geometry(ii_ctx* c, S0Geom* g) {
     g->ncol = (nch_in + g->group - 1) / g->group;
     return II_OK;
 }
+// The first pass's algorithmic bytes: 4 B per record of a narrow chunk (K1b
+// wrote u32 word slots there; two lanes share each 8-B load), 8 B per other
+// record, 8 B per kept record written.
+static uint64_t s0_bytes(uint64_t n_in, uint64_t n_narrow, uint64_t n_kept) {
+    n_narrow = std::min(n_narrow, n_in);
+    return 4 * n_narrow + 8 * (n_in - n_narrow) + 8 * n_kept;
+}
 template <bool kWid, bool kWideD, bool kHashD = false>
 static void sort0_inst(ii_ctx* c, const S0Geom& g, const uint64_t* k, uint64_t* k2, int shift, uint32_t dmask,
                        uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2, uint64_t* dhist) {
     k_sort0_compact<kWid, kWideD, kHashD><<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
         k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
-        (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files));
+        (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files),
+        P_<unsigned long long>(c->totals) + 8);
 }
 static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k, uint64_t* k2, int shift,
                          uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
@@ -464,14 +472,14 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
         if (passes) (*passes)++;
         if (first0) {  // sorted by the first digit, in *k: the rest runs over the kept records
             const uint64_t n_in = n;
-            uint64_t t47[4];
-            CK(read_u64(c, totals + 4, t47, 4));
+            uint64_t t47[5];
+            CK(read_u64(c, totals + 4, t47, 5));
             n = t47[0];
             if (wid) {  // exact wid range (k_count_hot wrote the occupied hot slots to totals[7])
                 c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));
                 hi = std::min(hi, lo + std::max(1, bitlen(c->NW - 1)));
             }
-            c->c0_bytes = 8 * n_in + 8 * n;
+            c->c0_bytes = s0_bytes(n_in, t47[4], n);
             if (ev) c->sc_bytes[c->n_sc - 1] = 16 * n;
             if (n_out) *n_out = n;
             if (n <= 1) break;
@@ -602,7 +610,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     k_msd_geometry<<<1, kRadix, 0, c->st>>>(table, (uint32_t)nch, nb, totals + 4, kSweepTile, bstart, btile, pad);
     HIPCK(hipMemsetAsync(gh, 0, sizeof(uint64_t) * 2 * nb * kRadix, c->st));
     HIPCK(hipGetLastError());
-    CK(read_queue(c, totals + 4, 4, 4));  // (kept count, wid range: read back while the scatter runs)
+    CK(read_queue(c, totals + 4, 4, 5));  // (kept count, wid range, narrow records: read while the scatter runs)
     // MSD scatter: u64 records -> u32 records in padded buckets
     const bool ev = c->n_sc + 3 <= kMaxTimedPasses;
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
@@ -621,12 +629,12 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     }
     if (ev) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
     HIPCK(hipGetLastError());
-    uint64_t t47[4];
-    CK(read_wait(c, t47, 4, 4));
+    uint64_t t47[5];
+    CK(read_wait(c, t47, 4, 5));
     const uint64_t n_in = n;
     n = t47[0];
     if (wid) c->NW = kHotSlots + (c->V - (t47[3] & 0xFFFFFFFFull));  // exact wid range (k_count_hot)
-    c->c0_bytes = 8 * n_in + 8 * n;
+    c->c0_bytes = s0_bytes(n_in, t47[4], n);
     *n_out = n;
     if (ev) c->sc_bytes[c->n_sc++] = 12 * n;
     *passes = 1;
@@ -926,7 +934,8 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
 
     // the separator contract, checked on the device (totals[9]); the host looks once, with the map's
     // other results
-    HIPCK(hipMemsetAsync(totals + 9, 0, sizeof(uint64_t), c->st));
+    // (totals[8]: the first sort pass's count of records in narrow chunks, zeroed with it)
+    HIPCK(hipMemsetAsync(totals + 8, 0, 2 * sizeof(uint64_t), c->st));
     k_check_layout<<<grid_for(c->nfiles), kBlock, 0, c->st>>>(c->text, fstart, c->nfiles, totals + 9);
     HIPCK(hipMemsetAsync(chunk_cnt + nch, 0, sizeof(uint64_t), c->st));  // voff[nch] = T after the scan
     c->rec_cap = use_fixed_capacity(c, nch, dense) ? kChunkCap : 0;

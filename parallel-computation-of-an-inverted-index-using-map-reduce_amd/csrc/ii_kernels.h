@@ -1518,7 +1518,8 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                                                            const uint32_t* __restrict__ remap,
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
                                                            int shift1, int shift2, uint64_t* __restrict__ dhist,
-                                                           const uint32_t* __restrict__ cf) {
+                                                           const uint32_t* __restrict__ cf,
+                                                           unsigned long long* __restrict__ narrow_recs) {
     constexpr int NT = kCBlock, NWv = kCWaves;
     constexpr int kTile = kCTile;
     constexpr uint32_t kBmWords = kDedupWords;
@@ -1540,6 +1541,12 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     for (uint32_t i = threadIdx.x; i <= ng; i += NT) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
     for (uint32_t i = threadIdx.x; i < ng; i += NT) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
     __syncthreads();
+    if (narrow_recs && w == 0) {  // records of this range read as u32 (narrow chunks): the pass's honest read bytes
+        uint32_t nr = 0;
+        for (uint32_t i = l; i < ng; i += 64) nr += s_cfid[i] != ~0u ? s_voff[i + 1] - s_voff[i] : 0u;
+        nr = wave_sum32(nr);
+        if (l == 0 && nr) atomicAdd(narrow_recs, (unsigned long long)nr);
+    }
     const uint64_t tofs = (uint64_t)w * 64 * kS0Items + l;
     const uint64_t lt = lanemask_lt();
     // this lane's chunk cursor (its indices only grow), all in registers so a

@@ -59,3 +59,51 @@ def test_full_size_index_matches_oracle(name):
         if share:
             assert st.sort_packed == 1
     assert not bad, "letters differ from the oracle: %s" % bad
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_logical_shards_full_size(G):
+    """BASELINE configs[3] at full size through the sharded path on one GPU:
+    the 10 GB config3 corpus cut by ii_partition (main.c:300-323, M = G) into
+    G contexts, each mapping and locally reducing its share with the files'
+    global ids; every context exports its letter segments, the owner of
+    ii_reducer_letters(r, G) (main.c:129-130) imports the G segments (the
+    merge-path owner merge, ~5*10^7 records per owner at G = 8) and formats
+    its letters.  The letters of all owners together must hash like the
+    oracle's index of the whole corpus (tests/golden/bench_hashes.json)."""
+    import torch
+    import ii_dist
+    w = DB["config3"]
+    p = w["iigen"]
+    idxs, bufs = [], []
+    try:
+        for g in range(G):
+            ids = share_ids(p, g, G)
+            text, off = ii_ctypes.zipf_shard(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], ids, threads=16)
+            n = int(off[-1])
+            d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+            d[:n].copy_(torch.from_numpy(text))
+            torch.cuda.synchronize()
+            del text
+            ix = ii_ctypes.Index(0)
+            idxs.append(ix)
+            bufs.append(d)
+            ix.map_device(d.data_ptr(), n, off[:-1].tolist(), ids)
+        los, his = ii_dist.logical_shards_reduce(idxs, p["nfiles"], copy_text=True)
+        got, words, out_bytes = {}, 0, 0
+        for g, ix in enumerate(idxs):
+            assert (los[g], his[g]) == ii_ctypes.reducer_letters(g, G)
+            for l in range(26):
+                t = ix.letter_text(l)
+                if los[g] <= l < his[g]:
+                    got[chr(97 + l)] = hashlib.sha256(t).hexdigest()
+                    words += t.count(b"\n")
+                    out_bytes += len(t)
+                else:
+                    assert t == b"", "owner %d holds letter %s it does not own" % (g, chr(97 + l))
+        assert words == w["words"] and out_bytes == w["out_bytes"]
+        bad = [l for l in w["letters"] if got.get(l) != w["letters"][l]["sha256"]]
+        assert not bad, "G=%d: letters differ from the oracle: %s" % (G, bad)
+    finally:
+        for ix in idxs:
+            ix.close()
