@@ -12,7 +12,8 @@
  * Ownership: the caller owns the file list, paths and input buffers; the
  * context owns every device and host buffer it allocates, including the
  * text returned by ii_letter_text (valid until the next ii_map_* / ii_reduce
- * call or ii_close).
+ * call, an export plan or letter load that follows ii_reduce — see
+ * ii_export_plan — or ii_close).
  * Errors: 0 = OK, negative = error code (ii_strerror).  Calls on one context
  * are not re-entrant; use one context per GPU.
  */
@@ -177,6 +178,11 @@ int ii_reduce_local(ii_ctx *ctx);
  *   u8  arena[arena_bytes rounded up to 8] = words in lexicographic order,
  *                    each followed by ' '
  * id_bound = 1 + the largest id0 of all files of all GPUs.
+ * Called after ii_reduce (whose token sort consumed the mapped records),
+ * ii_export_plan, ii_export_plan_ranges and ii_letter_load index the mapped
+ * input again: the text of the last ii_map_* call must still be valid (for
+ * ii_map_device, d_text), and the ii_letter_text results of that ii_reduce
+ * are invalidated (II_ERR_STATE until the next ii_reduce).
  */
 int ii_export_plan(ii_ctx *ctx, int nparts, uint64_t *seg_bytes);
 

@@ -168,6 +168,14 @@ static void note_hip_error(hipError_t e) {
     }
 }
 static inline bool poisoned() { return __atomic_load_n(&g_poisoned, __ATOMIC_SEQ_CST) != 0; }
+// A HIP result checked by hand (reader threads, timers, memory queries): true on
+// success; a failure is recorded like HIPCK's, so a sticky fault first seen
+// there still poisons the library.
+static inline bool hip_ok(hipError_t e) {
+    if (e == hipSuccess) return true;
+    note_hip_error(e);
+    return false;
+}
 
 #define HIPCK(x)                                                                               \
     do {                                                                                       \
@@ -198,9 +206,9 @@ static int grow(DBuf& b, size_t bytes) {
     b.p = nullptr;
     b.cap = 0;
     size_t want = std::max<size_t>(bytes + bytes / 8, 256);
-    if (hipMalloc(&b.p, want) != hipSuccess) {
+    if (!hip_ok(hipMalloc(&b.p, want))) {
         (void)hipGetLastError();
-        if (hipMalloc(&b.p, std::max<size_t>(bytes, 256)) != hipSuccess) {
+        if (!hip_ok(hipMalloc(&b.p, std::max<size_t>(bytes, 256)))) {
             (void)hipGetLastError();
             b.p = nullptr;
             return II_ERR_NOMEM;
@@ -872,7 +880,7 @@ static bool use_fixed_capacity(ii_ctx* c, uint64_t nch, bool dense) {
     if (e && !strcmp(e, "dense")) return false;
     if (e && !strcmp(e, "fixed")) return true;
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    if (!hip_ok(hipMemGetInfo(&fr, &tot))) {
         (void)hipGetLastError();
         return false;
     }
@@ -1173,18 +1181,18 @@ static void* io_worker(void* p) {
     IoJob* j = a->j;
     ii_ctx* c = j->c;
     int err = II_OK;
-    if (hipSetDevice(c->dev) != hipSuccess) err = II_ERR_HIP;
+    if (!hip_ok(hipSetDevice(c->dev))) err = II_ERR_HIP;
     int k = 0;
     for (uint64_t w = (uint64_t)a->t; err == II_OK && w < j->nwin; w += (uint64_t)j->nt, k ^= 1) {
         const int b = 2 * a->t + k;
-        if (hipEventSynchronize(c->io_ev[b]) != hipSuccess) { err = II_ERR_HIP; break; }  // buffer free again
+        if (!hip_ok(hipEventSynchronize(c->io_ev[b]))) { err = II_ERR_HIP; break; }  // buffer free again
         const uint64_t lo = w * kIoWin, hi = std::min(j->total, lo + kIoWin);
         io_fill(&j->lay, lo, hi, c->io_buf[b]);
-        if (hipMemcpyAsync(j->d_text + lo, c->io_buf[b], hi - lo, hipMemcpyHostToDevice, c->io_st[a->t]) != hipSuccess ||
-            hipEventRecord(c->io_ev[b], c->io_st[a->t]) != hipSuccess)
+        if (!hip_ok(hipMemcpyAsync(j->d_text + lo, c->io_buf[b], hi - lo, hipMemcpyHostToDevice, c->io_st[a->t])) ||
+            !hip_ok(hipEventRecord(c->io_ev[b], c->io_st[a->t])))
             err = II_ERR_HIP;
     }
-    if (err == II_OK && hipStreamSynchronize(c->io_st[a->t]) != hipSuccess) err = II_ERR_HIP;
+    if (err == II_OK && !hip_ok(hipStreamSynchronize(c->io_st[a->t]))) err = II_ERR_HIP;
     if (err != II_OK) {
         pthread_mutex_lock(&j->lay.mu);
         if (!j->err) j->err = err;
@@ -2080,7 +2088,7 @@ extern "C" int ii_device_text(ii_ctx* c, const uint8_t** d_text, uint64_t letter
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
     float ms = 0;
-    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    if (!hip_ok(hipEventElapsedTime(&ms, a, b))) {
         (void)hipGetLastError();
         return 0;
     }

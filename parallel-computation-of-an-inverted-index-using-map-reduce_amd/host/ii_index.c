@@ -44,20 +44,32 @@
 
 #define MAXG II_MAX_PARTS
 
-/* One GPU context of the multi-GPU CLI and its shard of files. */
+struct shard;
+/* What every context of a multi-GPU run shares: the letter owners (lo/hi,
+ * known before the map with the reference's split, after it with the
+ * balanced one), the exchange mode and, over RCCL, the communicator's id. */
 typedef struct {
-    int dev, nparts;
+    struct shard *sh;
+    int G, distinct, ranges_known;
+    int lo[MAXG], hi[MAXG];
+    ncclUniqueId nccl_id;
+} multi_run;
+
+/* One GPU context of the multi-GPU CLI and its shard of files. */
+typedef struct shard {
+    int g, dev, nparts;
     ii_ctx *ctx;
     ii_file *files;   /* the shard's files, ascending id0 */
     uint32_t n;
     uint32_t *local;  /* list index -> index in this shard (UINT32_MAX: another shard) */
     int nthreads;
     int rc;
+    multi_run *run;
+    uint64_t load[II_ALPHABET];  /* balanced split: distinct pairs per first letter of this shard */
     /* exchange: segment bytes for every owner, send / receive offsets */
     uint64_t seg[MAXG], send_off[MAXG + 1], recv_off[MAXG + 1];
     void *d_send, *d_recv;
     uint32_t id_bound;
-    hipStream_t st;
 } shard;
 
 /* ---- phases: one pthread per context, joined by run_phase.
@@ -78,22 +90,26 @@ typedef struct {
 
 typedef struct {
     shard *s;
-    int g;
+    int g, G;
     phase_sync *ps;
     void (*body)(shard *);
     const char *name;
 } phase_arg;
 
-static int test_fail_ctx(const char *phase) {
+/* the context II_TEST_FAIL names for this phase, or -1 (also for an index
+ * outside 0 .. G-1: a stray value must not block the CLI) */
+static int test_fail_ctx(const char *phase, int G) {
     const char *e = getenv("II_TEST_FAIL");
     size_t n = strlen(phase);
     if (!e || strncmp(e, phase, n) || e[n] != ':') return -1;
-    return atoi(e + n + 1);
+    char *end;
+    const long g = strtol(e + n + 1, &end, 10);
+    return end != e + n + 1 && *end == 0 && g >= 0 && g < G ? (int)g : -1;
 }
 
 static void *phase_thread(void *p) {
     phase_arg *a = p;
-    const int fail = test_fail_ctx(a->name);
+    const int fail = test_fail_ctx(a->name, a->G);
     if (fail == a->g) {
         a->s->rc = II_ERR_INTERNAL;
     } else if (fail >= 0) {
@@ -112,16 +128,16 @@ static void *phase_thread(void *p) {
 /* Run body on every context; II_OK once all succeeded (threads joined), or the
  * first error as soon as it is reported (the other threads are left alone). */
 static int run_phase(shard *sh, int G, void (*body)(shard *), const char *name) {
-    static phase_sync ps;
+    /* static: threads left behind by a failed phase still hold them (main() then exits); a phase
+     * starts only after the previous one joined all of its threads */
+    static phase_sync ps = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0};
     static phase_arg args[MAXG];
     pthread_t th[MAXG];
-    pthread_mutex_init(&ps.mu, NULL);
-    pthread_cond_init(&ps.cv, NULL);
     ps.done = 0;
     ps.err = II_OK;
     int started = 0;
     for (int g = 0; g < G; g++) {
-        args[g] = (phase_arg){&sh[g], g, &ps, body, name};
+        args[g] = (phase_arg){&sh[g], g, G, &ps, body, name};
         if (pthread_create(&th[g], NULL, phase_thread, &args[g]) != 0) {
             sh[g].rc = II_ERR_NOMEM;
             break;
@@ -138,13 +154,84 @@ static int run_phase(shard *sh, int G, void (*body)(shard *), const char *name) 
     return II_OK;
 }
 
+/* Export of one context: its segment for every owner into a device buffer of
+ * its own (ii_export waits for its copies: in this context's thread, so the G
+ * exports overlap). */
+static void export_body(shard *s) {
+    const multi_run *m = s->run;
+    s->rc = ii_export_plan_ranges(s->ctx, m->G, m->lo, m->hi, s->seg);
+    if (s->rc != II_OK) return;
+    s->send_off[0] = 0;
+    for (int r = 0; r < m->G; r++) s->send_off[r + 1] = s->send_off[r] + s->seg[r];
+    if (hipSetDevice(s->dev) != hipSuccess || hipMalloc(&s->d_send, s->send_off[m->G] + 8) != hipSuccess) {
+        s->d_send = NULL;
+        s->rc = II_ERR_NOMEM;
+        return;
+    }
+    s->rc = ii_export(s->ctx, m->G, s->d_send, s->send_off);
+}
+/* Map phase of one context: map + local reduce of its shard, then — when the
+ * letter owners are known up front (the reference's split) — its export; with
+ * the balanced split, its per-letter load instead. */
 static void map_body(shard *s) {
     s->rc = ii_open(&s->ctx, s->dev);
     if (s->rc == II_OK) s->rc = ii_map_files(s->ctx, s->files, s->n, s->nthreads, NULL);
-    if (s->rc == II_OK) s->rc = ii_reduce_local(s->ctx); /* lexid-keyed partial index, letter-contiguous */
+    if (s->rc == II_OK) s->rc = ii_reduce_local(s->ctx); /* distinct (word, file) pairs of the shard */
+    if (s->rc != II_OK) return;
+    if (s->run->ranges_known) export_body(s);
+    else s->rc = ii_letter_load(s->ctx, s->load);
+}
+/* Receive of owner g: segment g of every source into d_recv at recv_off[source].
+ * Over RCCL (a device per context) every context runs its own rank of one
+ * grouped ncclSend / ncclRecv round (point-to-point over xGMI: it sends its
+ * segments and receives its own); with shared devices the owner copies its
+ * segments from the sources' send buffers (device copies, all owners at once). */
+static int receive(shard *s) {
+    multi_run *m = s->run;
+    shard *sh = m->sh;
+    const int G = m->G, g = s->g;
+    if (hipSetDevice(s->dev) != hipSuccess) return II_ERR_HIP;
+    if (hipMalloc(&s->d_recv, s->recv_off[G] + 8) != hipSuccess) {
+        s->d_recv = NULL;
+        return II_ERR_NOMEM;
+    }
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return II_ERR_HIP;
+    int bad = 0;
+    if (m->distinct) {
+        ncclComm_t comm;
+        if (ncclCommInitRank(&comm, G, m->nccl_id, g) != ncclSuccess) {
+            (void)hipStreamDestroy(st);
+            return II_ERR_HIP;
+        }
+        bad |= ncclGroupStart() != ncclSuccess;
+        for (int r = 0; r < G && !bad; r++) {
+            if (s->seg[r]) /* my segment for owner r */
+                bad |= ncclSend((const char *)s->d_send + s->send_off[r], s->seg[r], ncclUint8, r, comm, st) !=
+                       ncclSuccess;
+            if (sh[r].seg[g]) /* source r's segment for me */
+                bad |= ncclRecv((char *)s->d_recv + s->recv_off[r], sh[r].seg[g], ncclUint8, r, comm, st) !=
+                       ncclSuccess;
+        }
+        bad |= ncclGroupEnd() != ncclSuccess;
+        bad |= hipStreamSynchronize(st) != hipSuccess;
+        ncclCommDestroy(comm);
+    } else {
+        for (int r = 0; r < G && !bad; r++) {
+            const uint64_t n = sh[r].seg[g];
+            if (n)
+                bad |= hipMemcpyPeerAsync((char *)s->d_recv + s->recv_off[r], s->dev,
+                                          (const char *)sh[r].d_send + sh[r].send_off[g], sh[r].dev, n, st) !=
+                       hipSuccess;
+        }
+        bad |= hipStreamSynchronize(st) != hipSuccess;
+    }
+    (void)hipStreamDestroy(st);
+    return bad ? II_ERR_HIP : II_OK;
 }
 static void merge_body(shard *s) {
-    s->rc = ii_import(s->ctx, s->nparts, s->d_recv, s->recv_off, s->id_bound);
+    s->rc = receive(s);
+    if (s->rc == II_OK) s->rc = ii_import(s->ctx, s->nparts, s->d_recv, s->recv_off, s->id_bound);
     if (s->rc == II_OK) s->rc = ii_reduce(s->ctx, 1);
 }
 
@@ -186,61 +273,25 @@ static int gpus_requested(void) {
     return g < 1 ? 1 : g > MAXG ? MAXG : g;
 }
 
-/* Move segment (g -> r) of every pair: one grouped RCCL round when every
- * shard has a device of its own (point-to-point over xGMI, all pairs at
- * once), device copies when shards share devices. */
-static int exchange(shard *sh, int G, int distinct) {
-    if (distinct) {
-        ncclComm_t comms[MAXG];
-        int devs[MAXG];
-        for (int g = 0; g < G; g++) devs[g] = sh[g].dev;
-        if (ncclCommInitAll(comms, G, devs) != ncclSuccess) return II_ERR_HIP;
-        int bad = 0;
-        for (int g = 0; g < G; g++) {
-            bad |= hipSetDevice(sh[g].dev) != hipSuccess;
-            bad |= hipStreamCreateWithFlags(&sh[g].st, hipStreamNonBlocking) != hipSuccess;
-        }
-        bad |= ncclGroupStart() != ncclSuccess;
-        for (int g = 0; g < G && !bad; g++)
-            for (int r = 0; r < G && !bad; r++) {
-                const uint64_t n = sh[g].seg[r];
-                if (!n) continue;
-                /* rank g sends its segment for owner r; owner r receives it at source g's offset */
-                bad |= ncclSend((const char *)sh[g].d_send + sh[g].send_off[r], n, ncclUint8, r, comms[g],
-                                sh[g].st) != ncclSuccess;
-                bad |= ncclRecv((char *)sh[r].d_recv + sh[r].recv_off[g], n, ncclUint8, g, comms[r],
-                                sh[r].st) != ncclSuccess;
-            }
-        bad |= ncclGroupEnd() != ncclSuccess;
-        for (int g = 0; g < G; g++) {
-            bad |= hipSetDevice(sh[g].dev) != hipSuccess;
-            bad |= hipStreamSynchronize(sh[g].st) != hipSuccess;
-            (void)hipStreamDestroy(sh[g].st);
-            ncclCommDestroy(comms[g]);
-        }
-        return bad ? II_ERR_HIP : II_OK;
-    }
-    for (int g = 0; g < G; g++)
-        for (int r = 0; r < G; r++) {
-            const uint64_t n = sh[g].seg[r];
-            if (!n) continue;
-            if (hipMemcpyPeer((char *)sh[r].d_recv + sh[r].recv_off[g], sh[r].dev,
-                              (const char *)sh[g].d_send + sh[g].send_off[r], sh[g].dev, n) != hipSuccess)
-                return II_ERR_HIP;
-        }
-    for (int g = 0; g < G; g++)
-        if (hipSetDevice(sh[g].dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return II_ERR_HIP;
-    return II_OK;
-}
-
-/* Multi-context index (G > 1), first half: shard the files, then map +
- * local reduce every shard (one pthread per context). */
-static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count, int M, int G, shard *sh) {
+/* Multi-context index (G > 1), first half: shard the files, then, one
+ * pthread per context, map + local reduce every shard and (reference split)
+ * export its segments.  The letter owners: the reference's reducer map with
+ * R = G (main.c:129-130), or with II_LETTER_SPLIT=balanced ranges balanced on
+ * the summed per-letter loads, known only after the maps. */
+static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count, int M, int G, shard *sh,
+                     multi_run *run) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
-        if (test_fail_ctx("map") < 0) return II_ERR_NODEV;
+        if (test_fail_ctx("map", G) < 0) return II_ERR_NODEV;
         ndev = 1; /* (the test knob's map phase opens no device: it runs without one) */
     }
+    run->sh = sh;
+    run->G = G;
+    run->distinct = ndev >= G;
+    const char *split = getenv("II_LETTER_SPLIT");
+    run->ranges_known = !(split && !strcmp(split, "balanced"));
+    if (run->ranges_known)
+        for (int r = 0; r < G; r++) ii_reducer_letters(r, G, &run->lo[r], &run->hi[r]); /* main.c:129-130 */
     uint32_t *order = calloc((size_t)count + 1, sizeof(uint32_t));
     uint32_t *shard_of = calloc((size_t)count + 1, sizeof(uint32_t));
     uint32_t sb[MAXG], se[MAXG];
@@ -248,6 +299,8 @@ static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count
     for (int g = 0; g < G; g++)
         for (uint32_t j = sb[g]; j < se[g]; j++) shard_of[order[j]] = (uint32_t)g;
     for (int g = 0; g < G; g++) {
+        sh[g].g = g;
+        sh[g].run = run;
         sh[g].dev = g % ndev;
         sh[g].nparts = G;
         sh[g].n = 0;
@@ -271,56 +324,32 @@ static int multi_map(const ii_file *files, const uint64_t *sizes, uint32_t count
     return run_phase(sh, G, map_body, "map");
 }
 
-/* Second half: letter owners, export, exchange, merge, order + format.
+/* Second half: (balanced split) letter owners and the exports, then one
+ * phase in which every context receives its segments (RCCL, or device copies
+ * when contexts share devices), merges them, orders and formats its letters.
  * owner[l] receives the context holding letter l.  The exchange buffers are
  * freed by the caller (multi_exchange), on every return. */
-static int multi_exchange_body(int G, shard *sh, ii_ctx **owner) {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return II_ERR_NODEV;
-    const int distinct = ndev >= G;
+static int multi_exchange_body(int G, shard *sh, multi_run *run, ii_ctx **owner) {
     int rc = II_OK;
-
-    /* letter owners */
-    int lo[MAXG], hi[MAXG];
-    const char *split = getenv("II_LETTER_SPLIT");
-    if (split && !strcmp(split, "balanced")) {
-        uint64_t load[II_ALPHABET] = {0}, part[II_ALPHABET];
-        for (int g = 0; g < G; g++) {
-            if ((rc = ii_letter_load(sh[g].ctx, part)) != II_OK) return rc;
-            for (int l = 0; l < II_ALPHABET; l++) load[l] += part[l];
-        }
-        if ((rc = ii_balanced_letters(load, G, lo, hi)) != II_OK) return rc;
-    } else {
-        for (int r = 0; r < G; r++) ii_reducer_letters(r, G, &lo[r], &hi[r]); /* main.c:129-130 */
+    if (!run->ranges_known) {
+        uint64_t load[II_ALPHABET] = {0};
+        for (int g = 0; g < G; g++)
+            for (int l = 0; l < II_ALPHABET; l++) load[l] += sh[g].load[l];
+        if ((rc = ii_balanced_letters(load, G, run->lo, run->hi)) != II_OK) return rc;
+        if ((rc = run_phase(sh, G, export_body, "export")) != II_OK) return rc;
     }
     for (int r = 0; r < G; r++)
-        for (int l = lo[r]; l < hi[r]; l++) owner[l] = sh[r].ctx;
-
-    /* plans, buffers, export */
-    for (int g = 0; g < G; g++) {
-        if ((rc = ii_export_plan_ranges(sh[g].ctx, G, lo, hi, sh[g].seg)) != II_OK) return rc;
-        sh[g].send_off[0] = 0;
-        for (int r = 0; r < G; r++) sh[g].send_off[r + 1] = sh[g].send_off[r] + sh[g].seg[r];
-    }
+        for (int l = run->lo[r]; l < run->hi[r]; l++) owner[l] = sh[r].ctx;
     for (int r = 0; r < G; r++) {
         sh[r].recv_off[0] = 0;
         for (int g = 0; g < G; g++) sh[r].recv_off[g + 1] = sh[r].recv_off[g] + sh[g].seg[r];
     }
-    for (int g = 0; g < G; g++) {
-        if (hipSetDevice(sh[g].dev) != hipSuccess) return II_ERR_HIP;
-        if (hipMalloc(&sh[g].d_send, sh[g].send_off[G] + 8) != hipSuccess ||
-            hipMalloc(&sh[g].d_recv, sh[g].recv_off[G] + 8) != hipSuccess)
-            return II_ERR_NOMEM;
-        if ((rc = ii_export(sh[g].ctx, G, sh[g].d_send, sh[g].send_off)) != II_OK) return rc;  /* synchronous */
-    }
-    if ((rc = exchange(sh, G, distinct)) != II_OK) return rc;
-
-    /* owners: merge the received segments, order + format (one thread per context) */
+    if (run->distinct && ncclGetUniqueId(&run->nccl_id) != ncclSuccess) return II_ERR_HIP;
     return run_phase(sh, G, merge_body, "merge");
 }
 
-static int multi_exchange(int G, shard *sh, ii_ctx **owner) {
-    const int rc = multi_exchange_body(G, sh, owner);
+static int multi_exchange(int G, shard *sh, multi_run *run, ii_ctx **owner) {
+    const int rc = multi_exchange_body(G, sh, run, owner);
     if (rc != II_OK) return rc; /* (no HIP call after a failure: main() exits) */
     for (int g = 0; g < G; g++) {
         (void)hipSetDevice(sh[g].dev);
@@ -520,6 +549,8 @@ int main(int argc, char **argv) {
     ii_ctx *single = NULL;
     shard sh[MAXG];
     memset(sh, 0, sizeof(sh));
+    multi_run run;
+    memset(&run, 0, sizeof(run));
     int rc, reported = 0;
     if (G == 1) {
         rc = ii_open(&single, 0);
@@ -534,10 +565,10 @@ int main(int argc, char **argv) {
             reported = 1;
         }
     } else {
-        rc = multi_map(files, sizes, (uint32_t)count, M, G, sh);
+        rc = multi_map(files, sizes, (uint32_t)count, M, G, sh, &run);
         /* partial files while the contexts still hold their input files (before the exchange) */
         if (rc == II_OK && partials) rc = write_partials(sh, G, NULL, order, nemit);
-        if (rc == II_OK) rc = multi_exchange(G, sh, owner);
+        if (rc == II_OK) rc = multi_exchange(G, sh, &run, owner);
     }
     int err = 0;
     if (rc != II_OK) {

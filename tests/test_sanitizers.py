@@ -152,6 +152,20 @@ def test_cli_failed_context_exits_promptly(cli, binary):
         assert marker not in err, err
 
 
+@pytest.mark.parametrize("knob", ["map:9", "map:-1", "map:", "map:2x", "merge:5"])
+def test_cli_stray_test_knob_is_ignored(cli, knob):
+    """II_TEST_FAIL naming no context of the phase (index outside
+    0 .. G-1, or not a number) must not block the CLI or skip its checks: here
+    (no GPU) it fails at once with the no-device error, as without the knob."""
+    with tempfile.TemporaryDirectory() as td:
+        write_list(td, make_files(td, 6))
+        env = dict(SAN_ENV, II_GPUS="5", II_TEST_FAIL=knob)
+        r = subprocess.run([cli, "2", "3", "list.txt"], cwd=td, capture_output=True, env=env, timeout=60)
+        err = r.stderr.decode(errors="replace")
+    assert r.returncode == 1, err
+    assert "no HIP device" in err, err
+
+
 @pytest.fixture(scope="module")
 def reader():
     subprocess.run(["make", "-C", PKG, "reader_san"], check=True, stdout=subprocess.DEVNULL)
