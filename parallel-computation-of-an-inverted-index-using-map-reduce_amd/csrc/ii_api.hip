@@ -537,21 +537,10 @@ static int run_sort32(ii_ctx* c, uint32_t** k, uint32_t** k2, uint64_t n, int bi
 // of up to kMsdMaxBits bits (k_msd_scatter_wide past kRadixBits).
 // II_PACKED_M=<m> (test knob): at least m top bits, so that small inputs reach
 // the wide split.
-// *one_pass: the bits left below the top digit are sorted in one pass
-// (k_bucket_lsd): the top digit takes at least W - kBkMaxBits bits when that
-// stays <= kMsdMaxBits (config3: m = 11, 10 low bits); II_LSD_ONE_PASS=0 (test
-// and A/B knob) keeps the two onesweep passes.
-static int packed_top_bits(int W, int F, bool* one_pass) {
-    *one_pass = false;
+static int packed_top_bits(int W, int F) {
     if (getenv("II_PACKED_SORT") && !strcmp(getenv("II_PACKED_SORT"), "0")) return 0;
     const char* fm = getenv("II_PACKED_M");
     const int m = std::max({7, W + F - 32, fm ? atoi(fm) : 0});
-    const char* op = getenv("II_LSD_ONE_PASS");
-    const int m1 = std::max(m, W - kBkMaxBits);
-    if (!(op && !strcmp(op, "0")) && m1 <= kMsdMaxBits && W - m1 >= 1) {
-        *one_pass = true;
-        return m1;
-    }
     const int L = W - m;
     return (m <= kMsdMaxBits && L >= 2 && L <= 2 * kRadixBits) ? m : 0;
 }
@@ -596,7 +585,7 @@ static constexpr size_t kMsdBytes = sizeof(uint64_t) * (3 * (size_t)kMsdMax + 2 
 // [lo, lo + W) of the records, ids below 2^F.  On return *k holds the *n_out
 // sorted records.
 static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, int lo, int W, int F, int m,
-                           bool one_pass, const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
+                           const uint32_t* remap0, uint64_t* n_out, bool wid, int* passes) {
     *passes = 0;
     *n_out = n;
     const uint32_t nb = 1u << m;
@@ -672,22 +661,6 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     CK(grow(c->tbk, sizeof(uint16_t) * ntb));
     uint16_t* tbk = P_<uint16_t>(c->tbk);
     k_tile_buckets<<<nb, kBlock, 0, c->st>>>(btile, tbk);
-    if (one_pass) {  // the low L bits in one pass, a workgroup per bucket (*k -> *k2, then swapped)
-        c->sort_hist_bytes = 0;
-        const bool evp = c->n_sc < kMaxTimedPasses;
-        if (evp) HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc], c->st));
-        k_bucket_lsd<kBkThreads, kBkItems, kBkMaxDig><<<nb, kBkThreads, 0, c->st>>>(
-            reinterpret_cast<const uint32_t*>(*k), reinterpret_cast<uint32_t*>(*k2), btile, bstart, F, L,
-            (uint32_t)kSweepTile);
-        if (evp) {
-            HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
-            c->sc_bytes[c->n_sc++] = 12 * n;  // the count read + one read + one write of u32 records
-        }
-        HIPCK(hipGetLastError());
-        std::swap(*k, *k2);
-        (*passes)++;
-        return II_OK;
-    }
     k_seg_hist<kSweepThreads, kSweepItems><<<hg, kSweepThreads, 0, c->st>>>(
         reinterpret_cast<const uint32_t*>(*k), btile, bstart, nb, per, F, b0, F + b0, b1, gh);
     k_digit_bases<<<2 * nb, kRadix, 0, c->st>>>(gh, gbase);
@@ -807,17 +780,8 @@ extern "C" int ii_open(ii_ctx** out, int device) {
     c->dev = device;
     HIPCK(hipSetDevice(device));
     HIPCK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
-#ifdef II_AB_PRIO
-    {
-        int least = 0, greatest = 0;
-        HIPCK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIPCK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, II_AB_PRIO == 2 ? 0 : greatest));
-        HIPCK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, least));
-    }
-#else
     HIPCK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HIPCK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
-#endif
     for (auto& e : c->ev) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_sc) HIPCK(hipEventCreate(&e));
     for (auto& e : c->ev_emit) HIPCK(hipEventCreate(&e));
@@ -1528,10 +1492,9 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     c->sort_packed = false;
     c->sort_W = lb;
     c->sort_F = F;
-    bool one_pass = false;
-    const int m = packed_top_bits(lb, F, &one_pass);
+    const int m = packed_top_bits(lb, F);
     if (m)
-        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, one_pass, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
+        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
                            &sort_passes));
     else
         CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,

@@ -1110,188 +1110,6 @@ __global__ __launch_bounds__(NT, 6) void k_onesweep_seg(const uint32_t* __restri
     }
 }
 
-// The packed layout's whole LSD sort in ONE pass when the key bits left below
-// the top digit fit one digit of up to kBkMaxBits bits (config3: W = 21 word-id
-// bits, an 11-bit top digit, 10 low bits): a workgroup per bucket walks the
-// bucket's records in order — stable by construction, so no look-back and no
-// global digit counts (k_seg_hist).  First it counts the bucket's digits (one
-// streaming read into LDS, four lane-interleaved copies), then, tile by tile,
-// ranks the tile's records by digit (ballot match + per-wave counts, as
-// k_onesweep_seg), reorders them in LDS and writes each digit's run behind the
-// digit's running cursor.  Against the two bucket-local onesweep passes and
-// k_seg_hist: one read + one write of the records instead of two, plus one
-// count read, and no look-back traffic.  Output: the same padded layout (K3
-// reads it).  The next tile's records are loaded while this tile is written.
-constexpr int kBkThreads = 512, kBkItems = 16, kBkTile = kBkThreads * kBkItems;
-constexpr int kBkMaxBits = 10, kBkMaxDig = 1 << kBkMaxBits;
-template <int NT, int IT, int NDIG>
-__global__ __launch_bounds__(NT, 4) void k_bucket_lsd(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
-                                                    const uint32_t* __restrict__ btile,
-                                                    const uint64_t* __restrict__ bstart, int shift, int dbits,
-                                                    uint32_t tile_pad) {
-    constexpr int NW = NT / 64;
-    constexpr int kTileN = NT * IT;
-    constexpr int DPT = NDIG / NT;  // digits owned by each thread (contiguous)
-    constexpr int kCopies = 4, kCStride = NDIG + 1;
-    static_assert(NDIG % NT == 0 && kCopies * kCStride <= NW * NDIG, "digit ownership / count copies");
-    __shared__ uint32_t s_keys[kTileN];
-    __shared__ uint32_t s_wcnt[NW][NDIG];  // per-wave digit counts -> offsets (count phase: the copies)
-    __shared__ uint32_t s_run[NDIG];       // bucket-relative output cursor of every digit
-    __shared__ uint32_t s_tstart[NDIG];    // tile-relative start of every digit
-    __shared__ uint32_t s_scan[NW];
-
-    const int w = wave_id(), l = lane_id(), t = threadIdx.x;
-    const uint32_t h = blockIdx.x;
-    const uint64_t base = (uint64_t)btile[h] * tile_pad;
-    const uint32_t cnt = (uint32_t)(bstart[h + 1] - bstart[h]);
-    if (cnt == 0) return;  // (workgroup-uniform)
-    const uint32_t dmask = (1u << dbits) - 1u;
-    const uint32_t* in = kin + base;
-    uint32_t* out = kout + base;
-
-    // the first tile's records, in flight while the digits are counted
-    const uint32_t wrel = (uint32_t)w * 64 * IT + (uint32_t)l;
-    uint32_t key[IT];
-#pragma unroll
-    for (int k = 0; k < IT; k++) key[k] = wrel + k * 64 < cnt ? in[wrel + k * 64] : ~0u;
-
-    // 1. digit counts of the bucket
-    uint32_t* hc = &s_wcnt[0][0];
-    for (int i = t; i < kCopies * kCStride; i += NT) hc[i] = 0;
-    __syncthreads();
-    {
-        uint32_t* c = hc + (l & (kCopies - 1)) * kCStride;
-        const uint32_t n4 = cnt & ~3u;
-        for (uint32_t i0 = 4 * t; i0 < n4; i0 += 16 * NT) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t i = i0 + 4 * NT * u;
-                v[u] = i < n4 ? *reinterpret_cast<const uint4*>(in + i) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (i0 + 4 * NT * u < n4) {
-                    atomicAdd(&c[(v[u].x >> shift) & dmask], 1u);
-                    atomicAdd(&c[(v[u].y >> shift) & dmask], 1u);
-                    atomicAdd(&c[(v[u].z >> shift) & dmask], 1u);
-                    atomicAdd(&c[(v[u].w >> shift) & dmask], 1u);
-                }
-            }
-        }
-        if ((uint32_t)t < cnt - n4) atomicAdd(&c[(in[n4 + t] >> shift) & dmask], 1u);
-    }
-    __syncthreads();
-    {  // exclusive scan over the digits (thread t owns digits [t * DPT, + DPT)) -> s_run
-        uint32_t dc[DPT], sum = 0;
-#pragma unroll
-        for (int j = 0; j < DPT; j++) {
-            const int d = t * DPT + j;
-            uint32_t a = 0;
-#pragma unroll
-            for (int cp = 0; cp < kCopies; cp++) a += hc[cp * kCStride + d];
-            dc[j] = a;
-            sum += a;
-        }
-        const uint32_t inc = wave_incl_scan32(sum);
-        if (l == 63) s_scan[w] = inc;
-        __syncthreads();
-        uint32_t run = inc - sum;
-        for (int ww = 0; ww < w; ww++) run += s_scan[ww];
-#pragma unroll
-        for (int j = 0; j < DPT; j++) {
-            s_run[t * DPT + j] = run;
-            run += dc[j];
-        }
-    }
-    uint32_t tot[DPT];  // this tile's count of every owned digit (added to s_run once the tile is written)
-#pragma unroll
-    for (int j = 0; j < DPT; j++) tot[j] = 0;
-    const uint64_t lt = lanemask_lt();
-    for (uint32_t tb = 0; tb < cnt; tb += kTileN) {
-        __syncthreads();  // the previous tile's writers are done with s_run, s_tstart, s_keys, s_wcnt
-#pragma unroll
-        for (int j = 0; j < DPT; j++) s_run[t * DPT + j] += tot[j];
-#pragma unroll
-        for (int ww = 0; ww < NW; ww++)
-#pragma unroll
-            for (int j = 0; j < DPT; j++) s_wcnt[ww][t * DPT + j] = 0;
-        __syncthreads();
-        // 2. rank every record of the tile among its digit (wave order, then item order, then lane)
-        const uint32_t vrel = cnt - tb < (uint32_t)kTileN ? cnt - tb : (uint32_t)kTileN;
-        uint32_t rank[IT];
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const bool valid = wrel + (uint32_t)k * 64 < vrel;
-            const uint32_t d = (key[k] >> shift) & dmask;
-            uint64_t m = __ballot(valid);
-#pragma unroll
-            for (int b = 0; b < kBkMaxBits; b++) {
-                if (b < dbits) {
-                    const bool bit = (d >> b) & 1;
-                    const uint64_t bb = __ballot(bit);
-                    m &= bit ? bb : ~bb;
-                }
-            }
-            const uint32_t below = (uint32_t)__popcll(m & lt);
-            const int leader = valid ? __builtin_ctzll(m) : 0;
-            uint32_t before = 0;
-            if (valid && below == 0) before = atomicAdd(&s_wcnt[w][d], (uint32_t)__popcll(m));
-            rank[k] = (uint32_t)__shfl((int)before, leader, 64) + below;
-        }
-        __syncthreads();
-        // 3. tile-relative digit starts; per-wave counts -> the wave's first slot in its digit
-        {
-            uint32_t sum = 0;
-#pragma unroll
-            for (int j = 0; j < DPT; j++) {
-                uint32_t a = 0;
-#pragma unroll
-                for (int ww = 0; ww < NW; ww++) a += s_wcnt[ww][t * DPT + j];
-                tot[j] = a;
-                sum += a;
-            }
-            const uint32_t inc = wave_incl_scan32(sum);
-            if (l == 63) s_scan[w] = inc;
-            __syncthreads();
-            uint32_t st = inc - sum;
-            for (int ww = 0; ww < w; ww++) st += s_scan[ww];
-#pragma unroll
-            for (int j = 0; j < DPT; j++) {
-                const int d = t * DPT + j;
-                s_tstart[d] = st;
-                uint32_t o = st;
-#pragma unroll
-                for (int ww = 0; ww < NW; ww++) {
-                    const uint32_t c = s_wcnt[ww][d];
-                    s_wcnt[ww][d] = o;
-                    o += c;
-                }
-                st += tot[j];
-            }
-        }
-        __syncthreads();
-        // 4. reorder in LDS, then the next tile's records are loaded while this one is written
-#pragma unroll
-        for (int k = 0; k < IT; k++)
-            if (wrel + (uint32_t)k * 64 < vrel) s_keys[s_wcnt[w][(key[k] >> shift) & dmask] + rank[k]] = key[k];
-        __syncthreads();
-        const uint32_t nb0 = tb + kTileN;
-#pragma unroll
-        for (int k = 0; k < IT; k++) key[k] = nb0 + wrel + k * 64 < cnt ? in[nb0 + wrel + k * 64] : ~0u;
-        // 5. write: every digit's run of the tile behind the digit's cursor
-#pragma unroll
-        for (int j = 0; j < IT; j++) {
-            const uint32_t p = j * NT + t;
-            if (p < vrel) {
-                const uint32_t k = s_keys[p];
-                const uint32_t d = (k >> shift) & dmask;
-                out[s_run[d] + (p - s_tstart[d])] = k;
-            }
-        }
-    }
-}
-
 // dbase[r * kRadix + d] = exclusive prefix over digits of dhist[r * kRadix + d]
 // (one workgroup per row).
 __global__ __launch_bounds__(kRadix) void k_digit_bases(const uint64_t* __restrict__ dhist, uint64_t* __restrict__ dbase) {

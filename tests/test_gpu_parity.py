@@ -441,29 +441,23 @@ def test_packed_sort_forms_vs_oracle():
     off = off.tolist()
     for ids, packed in [(list(range(700)), 1), ([700 * i for i in range(700)], 1), ([6007 * i for i in range(700)], 1)]:
         exp = oracle_index(t, off, ids)
-        # default: the one-pass bucket LSD (k_bucket_lsd: MSD + 1 pass); II_LSD_ONE_PASS=0: MSD + two
-        # bucket-local onesweep passes; II_PACKED_SORT=0: the u64 passes
-        for env, passes in [({}, 2), ({"II_LSD_ONE_PASS": "0"}, 3), ({"II_PACKED_SORT": "0"}, None)]:
-            os.environ.update(env)
+        for env in [None, "0"]:
+            if env is not None:
+                os.environ["II_PACKED_SORT"] = env
             try:
                 with ii_ctypes.Index(0) as ix:
                     ix.map_host(t, off, ids)
                     ix.reduce()
-                    assert_same(ix.letters(), exp, "ids up to %d, %s" % (ids[-1], env))
+                    assert_same(ix.letters(), exp, "ids up to %d, II_PACKED_SORT=%s" % (ids[-1], env))
                     st = ix.stats()
-                    assert st.sort_packed == (packed if passes else 0)
-                    if passes:
-                        assert st.sort_passes == passes, (env, st.sort_passes)
+                    assert st.sort_packed == (packed if env is None else 0)
                     assert st.sort_bytes > 0
             finally:
-                for k in env:
-                    os.environ.pop(k, None)
+                os.environ.pop("II_PACKED_SORT", None)
 
 
 @pytest.mark.parametrize("env", [{"II_PACKED_M": "9"}, {"II_PACKED_M": "10"}, {"II_PACKED_M": "11"},
-                                 {"II_PACKED_M": "10", "II_SORT_KEYS": "lexid"},
-                                 {"II_PACKED_M": "9", "II_LSD_ONE_PASS": "0"},
-                                 {"II_PACKED_M": "11", "II_LSD_ONE_PASS": "0"}])
+                                 {"II_PACKED_M": "10", "II_SORT_KEYS": "lexid"}])
 def test_wide_top_digit_vs_oracle(env):
     """The token sort's wide top digit (II_PACKED_M forces m top bits: the
     wide MSD split k_msd_scatter and k_sort0_compact's wide count row, the form
