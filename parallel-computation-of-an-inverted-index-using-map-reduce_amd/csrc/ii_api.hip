@@ -51,7 +51,10 @@ struct ii_ctx {
     uint64_t nbytes = 0;
     uint32_t nfiles = 0;
     uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df)
-    bool fid_ident = true;  // the mapped files' id0s are 0, 1, 2, ... (K1's shard-local file index == id0)
+    // the mapped files' id0s are fid_off, fid_off + 1, ... (a contiguous range, as ii_partition's
+    // shares are): K3 adds fid_off to K1's shard-local file index instead of gathering fid[index]
+    bool fid_affine = true;
+    uint32_t fid_off = 0;
     IdDigitsTh dth{};       // K3's posting bytes by file index (pair_bytes)
     DBuf fstart, fid;
     std::vector<uint64_t> h_fstart;  // host copies of the mapped files' starts / ids
@@ -688,9 +691,9 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
 // K3: distinct (lexid, id0) pairs of the sorted records r[0, n), their
 // posting byte offsets (P[U] = all posting bytes) and each word's first pair
 // (post_start[V] = U).  Sets c->U.  fmap: id0 of every shard-local file index
-// the records carry (null: the records carry id0s).
+// the records carry (null: the records carry id0 - fid_off).
 static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool packed, const uint32_t* fmap,
-                      bool compact) {
+                      bool compact, uint32_t fid_off = 0) {
     c->xpairs = false;
     if (compact && c->id_bound > kPairFirst) compact = false;  // (the top bit marks a word's first pair: u64 pairs)
     c->pairs32 = compact;
@@ -737,14 +740,14 @@ static int run_unique(ii_ctx* c, const uint64_t* r, uint64_t n, bool wid, bool p
         (fmap ? k_uniq_sweep<true, true> : k_uniq_sweep<true, false>)<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             nullptr, n, reinterpret_cast<const uint32_t*>(r), c->pk_ncap, btile, P_<uint16_t>(c->tbk), bstart, c->pk_nb, c->pk_F, c->pk_L, uniq, Pp, ps_k,
             pe_k, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6,
-            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64, c->dth);
+            P_<unsigned long long>(c->counters) + C_OVERFLOW, fmap, u32, g64, c->dth, fid_off);
     } else {
         const uint64_t ntiles = (n + kUniqSweepTile - 1) / kUniqSweepTile;
         CK(lookback_pass(c, 2 * ntiles));
         (fmap ? k_uniq_sweep<false, true> : k_uniq_sweep<false, false>)<<<(uint32_t)ntiles, kBlock, 0, c->st>>>(
             r, n, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, uniq, Pp, ps_k, pe_k, P_<uint64_t>(c->lbstat),
             P_<uint32_t>(c->ticket), c->lb_epoch, ps + c->V, totals + 6, P_<unsigned long long>(c->counters) + C_OVERFLOW,
-            fmap, u32, g64, c->dth);
+            fmap, u32, g64, c->dth, fid_off);
         k_post_last<<<1, 64, 0, c->st>>>(r, n, ps + c->V, pe_k);
     }
     // K3's look-back flags kLbTimeout instead of hanging (a predecessor tile that never
@@ -1086,7 +1089,9 @@ static int set_files(ii_ctx* c, const uint64_t* file_start, const uint32_t* file
     }
     c->nfiles = nfiles;
     c->id_bound = nfiles ? file_id0[nfiles - 1] + 1 : 0;
-    c->fid_ident = !nfiles || file_id0[nfiles - 1] == nfiles - 1;  // ascending ids: the last is nfiles - 1 iff all are i
+    // ascending ids: the last is first + nfiles - 1 iff they are consecutive
+    c->fid_affine = !nfiles || file_id0[nfiles - 1] - file_id0[0] == nfiles - 1;
+    c->fid_off = nfiles ? file_id0[0] : 0u;
     c->h_fstart.assign(file_start, file_start + nfiles);
     c->h_fid.assign(file_id0, file_id0 + nfiles);
     for (int k = 0; k < 9; k++) {  // the first file index whose id0 + 1 >= 10^(k + 1)
@@ -1538,7 +1543,8 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
         HIPCK(hipMemcpyAsync(c->hbuf, P_<uint64_t>(c->counters) + C_COLLIDE, sizeof(uint64_t), hipMemcpyDeviceToHost,
                              c->st));
     }
-    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_ident ? nullptr : P_<uint32_t>(c->fid), compact));
+    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_affine ? nullptr : P_<uint32_t>(c->fid), compact,
+                  c->fid_affine ? c->fid_off : 0u));
     if (check) {
         c->lv_pending = false;
         if (c->hbuf[0]) {  // (Las Vegas: the output never depends on the seed)

@@ -858,12 +858,15 @@ struct HotProbe {
 // The probe for vocabularies larger than the hot level (DeepProbe, chosen by
 // the host when most of the previous map's distinct words lived in the big
 // table — configs[4]'s vocabulary of 10^7 against 2^20 hot slots): a lane
-// whose two pairs are full without its key loads the bucket's other two pairs
-// and its big-table home slot in one more round trip, so a word resolved at
-// its big home (found, or claimed there: table_find's rule, whose linear
-// probe starts at the home) no longer goes to the K1c tail; only words past
-// their big home do.  (With a vocabulary that fits the hot level the extra
-// round trip costs more than the few K1c tokens it saves: emit +0.2 ms at 10 GB.)
+// whose home pair is full without its key loads the bucket's other three
+// pairs and its big-table home slot in one more round trip, so a word
+// resolved at its big home (found, or claimed there: table_find's rule, whose
+// linear probe starts at the home) no longer goes to the K1c tail; only words
+// past their big home do.  (With a vocabulary that fits the hot level the
+// extra round trip costs more than the few K1c tokens it saves: emit +0.2 ms
+// at 10 GB.  Round 5: the second pair in the same round trip as the rest of
+// the bucket instead of one of its own, emit 22.47 -> 21.83 ms on the rank-7
+// share of configs[4]: nearly every batch has a lane past its home pair.)
 struct DeepProbe {
     __device__ __forceinline__ ProbeState begin(const Table& t, bool fast, uint64_t key, uint32_t home) const {
         return HotProbe().begin(t, fast, key, home);
@@ -873,16 +876,14 @@ struct DeepProbe {
         const uint32_t bbase = st.home & ~(uint32_t)(kBucket - 1), start = st.home & (kBucket - 2);
         uint32_t match = (uint32_t)(st.qa.x == key) | ((uint32_t)(st.qa.y == key) << 1);
         uint32_t empty = (uint32_t)(st.qa.x == 0ull) | ((uint32_t)(st.qa.y == 0ull) << 1);
-        if (fast && !(match | empty)) {
-            const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
-            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
-            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
-        }
-        if (fast && !(match | empty)) {  // the bucket's other two pairs and the big-table home, one round trip
+        if (fast && !(match | empty)) {  // the bucket's other three pairs and the big-table home, one round trip
             const uint64_t h = big_home(t, key);
+            const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 2) & (kBucket - 2)));
             const ulonglong2 qc = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 4) & (kBucket - 2)));
             const ulonglong2 qd = *reinterpret_cast<const ulonglong2*>(t.keys + bbase + ((start + 6) & (kBucket - 2)));
             const unsigned long long kb = t.keys[kHotSlots + h];
+            match |= ((uint32_t)(qb.x == key) << 2) | ((uint32_t)(qb.y == key) << 3);
+            empty |= ((uint32_t)(qb.x == 0ull) << 2) | ((uint32_t)(qb.y == 0ull) << 3);
             match |= ((uint32_t)(qc.x == key) << 4) | ((uint32_t)(qc.y == key) << 5) | ((uint32_t)(qd.x == key) << 6) |
                      ((uint32_t)(qd.y == key) << 7);
             empty |= ((uint32_t)(qc.x == 0ull) << 4) | ((uint32_t)(qc.y == 0ull) << 5) | ((uint32_t)(qd.x == 0ull) << 6) |
@@ -1898,7 +1899,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                                                        uint64_t epoch, uint64_t* __restrict__ U_out,
                                                        uint64_t* __restrict__ B_out, unsigned long long* __restrict__ err,
                                                        const uint32_t* __restrict__ fmap, uint32_t* __restrict__ uniq32,
-                                                       uint32_t* __restrict__ g64, IdDigitsTh dth) {
+                                                       uint32_t* __restrict__ g64, IdDigitsTh dth, uint32_t fid_off) {
     // the tile staged in LDS (scanned, then written after the look-back): u64
     // records from [1] with the record before the tile at [0], or in the packed
     // form the raw u32 records (16 KiB, 8 workgroups per CU instead of 3) and
@@ -1994,7 +1995,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
             const uint64_t i = lo + (uint64_t)k * kUniqTile + (uint64_t)q * kBlock + t;
             if (i < hi && r != pv) {  // (pv = ~0 before the first record: never a record)
                 c8 |= 1u << (8 * q);
-                const uint32_t d = pair_bytes(kFmap ? fmap : nullptr, dth, (uint32_t)r);
+                const uint32_t d = pair_bytes(kFmap ? fmap : nullptr, dth, (uint32_t)r + (kFmap ? 0u : fid_off));
                 if (q < 2) bl += d << (16 * q);
                 else bh += d << (16 * (q - 2));
                 tcount++;
@@ -2127,7 +2128,7 @@ __global__ __launch_bounds__(kBlock, kPacked ? 8 : 4) void k_uniq_sweep(const ui
                 const uint64_t uu = rc + (f & 0x7FFFull);
                 const uint32_t key = (uint32_t)(r >> 32), pkey = (uint32_t)(pv >> 32);
                 const bool wstart = pv == ~0ull || key != pkey;
-                const uint32_t id0 = !kFmap ? (uint32_t)r
+                const uint32_t id0 = !kFmap ? (uint32_t)r + fid_off
                                    : k == 0 ? gid[q] : k == 1 ? gid[kUniqItems + q]
                                    : k == 2 ? gid[2 * kUniqItems + q] : gid[3 * kUniqItems + q];
                 if (uniq32) {  // (uniform)
@@ -2230,11 +2231,15 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
     uint32_t len = lex_len[j];
     // posting p of word j starts at fbase[key(j)] + P[p] (key = wid or lexid):
     // one gather per posting in k_fmt_posts instead of four
-    fbase[widl ? widl[j] : j] = o + len + 2 - P[post_start[j]];
-    write_word(text, nbytes, lex_key[j], lex_rep[j], len, out + o);
+    // every load before the first store: a load issued after a store waits for it too (vmcnt counts both)
+    const uint64_t ps = P[post_start[j]], pe = P[post_end[j]];
+    const uint64_t key = lex_key[j], rep = lex_rep[j];
+    const uint32_t wl = widl ? widl[j] : j;
+    fbase[wl] = o + len + 2 - ps;
+    out[o + len + 3 + (pe - ps) - 1] = '\n';
+    write_word(text, nbytes, key, rep, len, out + o);
     out[o + len] = ':';
     out[o + len + 1] = '[';
-    out[o + len + 3 + (P[post_end[j]] - P[post_start[j]]) - 1] = '\n';
 }
 
 // uniq keys are wids or lexids, fbase is indexed the same way (k_fmt_words).

@@ -146,6 +146,18 @@ def test_noncontiguous_ids(idx):
     assert_same(idx.letters(), oracle_index(text, off, ids), "ids")
 
 
+@pytest.mark.parametrize("first", [1, 95, 9999980, 4294967200])
+def test_offset_contiguous_ids(idx, first):
+    # an ii_partition share: consecutive ids from `first` (K3 adds the offset to the shard-local
+    # file index instead of gathering the id), across digit-count boundaries and past 2^31
+    # (u64 pairs instead of the compact form)
+    text, off, _ = rand_corpus(11, 40, 5000)
+    ids = [first + i for i in range(40)]
+    idx.map_host(text, off, ids)
+    idx.reduce()
+    assert_same(idx.letters(), oracle_index(text, off, ids), "first %d" % first)
+
+
 def long_variant_corpus(seed, nfiles=60, per_file=3000):
     """Long words (13-120 letters) written many ways: case changes, digits,
     punctuation, high bytes and NULs inside, so that most occurrences differ
