@@ -15,8 +15,8 @@
 #   xchg[:G]               tools/exchange_timing.py 1.25e9 G 3 1 corpus (G = 8), kernel trace
 #   sortbench              tools/sort_bench (onesweep pass vs copy vs rocPRIM)
 #   listpmc                rocprofv3 -L (the counters of this GPU)
-#   sq[:REGEX]             SQ counter passes (tools/gpu_pmc.sh) over a short bench, kernels matching REGEX
-#                          (default k_tok_emit|k_sort0_compact)
+#   sq[:REGEX[:ARGS]]      SQ counter passes (tools/gpu_pmc.sh) over a short bench (+ARGS), kernels
+#                          matching REGEX (default k_tok_emit|k_sort0_compact)
 # Example:  gpu_session.sh r5a tests prof sortbench
 set -o pipefail
 TAG=${1:?tag}
@@ -80,12 +80,15 @@ step() {
     sortbench)
         timeout -k 10 300 "$PKG/sort_bench" > "$OUT/sort_bench.log" 2>&1 && cat "$OUT/sort_bench.log" ;;
     sq)
-        bash "$T/gpu_pmc.sh" "$OUT/sq" "${arg:-k_tok_emit|k_sort0_compact}" \
+        local rx=${arg%%:*} bargs=""
+        [ "$arg" != "$rx" ] && bargs=${arg#*:}
+        # shellcheck disable=SC2086
+        bash "$T/gpu_pmc.sh" "$OUT/sq" "${rx:-k_tok_emit|k_sort0_compact}" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
             "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT" \
             "SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_LDS_ATOMIC" \
             "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_BUBBLE_sum" \
-            -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify ;;
+            -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify $bargs ;;
     listpmc)
         timeout -k 10 120 rocprofv3 -L > "$OUT/rocprofv3_L.txt" 2>&1 && echo "listed $(wc -l < "$OUT/rocprofv3_L.txt") lines" ;;
     *)
