@@ -51,8 +51,8 @@ struct ii_ctx {
     uint64_t nbytes = 0;
     uint32_t nfiles = 0;
     uint32_t id_bound = 0;  // 1 + largest file id0 (bounds df)
-    // the mapped files' id0s are fid_off, fid_off + 1, ... (a contiguous range, as ii_partition's
-    // shares are): K3 adds fid_off to K1's shard-local file index instead of gathering fid[index]
+    // the mapped files' id0s are fid_off, fid_off + 1, ... (a caller's id range; ii_partition's size-sorted
+    // shares are not): K3 adds fid_off to K1's shard-local file index instead of gathering fid[index]
     bool fid_affine = true;
     uint32_t fid_off = 0;
     IdDigitsTh dth{};       // K3's posting bytes by file index (pair_bytes)
