@@ -1795,7 +1795,7 @@ extern "C" int ii_export(ii_ctx* c, int nparts, void* d_send, const uint64_t* se
         HIPCK(hipGetLastError());
     }
     if (c->wid_pairs && c->U) {  // every part's pairs in one pass over the word-id order
-        k_export_pairs_wid<<<(uint32_t)std::min<uint64_t>(16384, grid_for(c->U)), kBlock, 0, c->st>>>(
+        k_export_pairs_wid<<<(uint32_t)std::min<uint64_t>(16384, grid_for((c->U + kExportItems - 1) / kExportItems)), kBlock, 0, c->st>>>(
             P_<uint64_t>(c->uniq), c->U, P_<uint32_t>(c->lexw), P_<uint64_t>(c->pstart), P_<uint64_t>(c->pstart_x), xp);
         HIPCK(hipGetLastError());
     }

@@ -2440,6 +2440,7 @@ __global__ __launch_bounds__(kBlock) void k_export_words(const uint8_t* __restri
 // as (j - j0) << 32 | id0 at dst + that index - the part's first pair.  (The
 // copy, k_pairs_by_lexid, wrote and re-read 16 bytes a pair more.)
 constexpr int kExportMaxParts = 64;  // II_MAX_PARTS
+constexpr int kExportItems = 4;      // pairs per thread per step of k_export_pairs_wid
 struct ExportParts {
     uint32_t n;
     uint32_t j0[kExportMaxParts + 1];  // first lexid of part r (j0[n] = V)
@@ -2461,16 +2462,38 @@ __global__ __launch_bounds__(kBlock) void k_export_pairs_wid(const uint64_t* __r
         }
     }
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < U; i += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t rr = uniq[i];
-        const uint32_t j = lexw[rr >> 32];
-        uint32_t lo = 0, hi = parts.n - 1;  // the last part with j0 <= j
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) / 2;
-            if (s_j0[mid] <= j) lo = mid;
-            else hi = mid - 1;
+    // kExportItems pairs per thread per step, each of the three dependent loads
+    // (pair, word's lexid, its offsets) issued for all of them before the next:
+    // one chain of three round trips per kExportItems pairs instead of per pair
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i0 < U; i0 += kExportItems * stride) {
+        uint64_t rr[kExportItems], px[kExportItems], pw[kExportItems];
+        uint32_t j[kExportItems];
+#pragma unroll
+        for (int q = 0; q < kExportItems; q++) {
+            const uint64_t i = i0 + q * stride;
+            rr[q] = i < U ? uniq[i] : 0ull;
         }
-        s_dst[lo][psx[j] + (i - ps[j]) - s_p0[lo]] = ((uint64_t)(j - s_j0[lo]) << 32) | (rr & 0xFFFFFFFFull);
+#pragma unroll
+        for (int q = 0; q < kExportItems; q++) j[q] = i0 + q * stride < U ? lexw[rr[q] >> 32] : 0u;
+#pragma unroll
+        for (int q = 0; q < kExportItems; q++) {
+            const bool ok = i0 + q * stride < U;
+            px[q] = ok ? psx[j[q]] : 0ull;
+            pw[q] = ok ? ps[j[q]] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < kExportItems; q++) {
+            const uint64_t i = i0 + q * stride;
+            if (i >= U) continue;
+            uint32_t lo = 0, hi = parts.n - 1;  // the last part with j0 <= j
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (s_j0[mid] <= j[q]) lo = mid;
+                else hi = mid - 1;
+            }
+            s_dst[lo][px[q] + (i - pw[q]) - s_p0[lo]] = ((uint64_t)(j[q] - s_j0[lo]) << 32) | (rr[q] & 0xFFFFFFFFull);
+        }
     }
 }
 
