@@ -2339,16 +2339,21 @@ __global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restr
             const bool last = p + 1 == U || (k32 ? wn[k] != 0u : wn[k] != (uint32_t)(r[k] >> 32));
             const uint64_t o = fb[k] + pb[k] + (inc - len);
             if (nd <= 7u) {
-                // digits + separator (<= 8 bytes) built in one register (each lower digit pushes
-                // the bytes after it up one place), then stored with at most three sized stores
-                // (unaligned global stores are native on gfx950): one byte store per digit made
-                // the pass issue-bound
-                uint64_t s = (uint64_t)(last ? ']' : ' ');
-                uint32_t v = (uint32_t)id;
-                for (uint32_t i = 0; i < nd; i++) {
-                    s = (s << 8) | (uint64_t)('0' + v % 10u);
-                    v /= 10u;
-                }
+                // digits + separator (<= 8 bytes) built in one register, then stored with at most
+                // three sized stores (unaligned global stores are native on gfx950): one byte store
+                // per digit made the pass issue-bound.
+                // The 8 decimal digits of id (< 10^7 here, leading zeros) by SWAR: two 4-digit
+                // halves, each split into 2-digit 16-bit lanes, each lane into a tens / ones byte
+                // (multiply-shift divisions exact below 10^4 and 10^2), then the leading zeros shifted
+                // out — straight-line VALU instead of a loop of nd divisions by 10
+                const uint32_t v = (uint32_t)id, vh = v / 10000u, vl = v - vh * 10000u;
+                const uint32_t hh = (vh * 10486u) >> 20, lh = (vl * 10486u) >> 20;
+                uint32_t A = hh | ((vh - hh * 100u) << 16), B = lh | ((vl - lh * 100u) << 16);
+                const uint32_t Az = ((A * 103u) >> 10) & 0x000F000Fu, Bz = ((B * 103u) >> 10) & 0x000F000Fu;
+                A = Az | ((A - Az * 10u) << 8);
+                B = Bz | ((B - Bz * 10u) << 8);
+                const uint64_t dig = (((uint64_t)B << 32) | A) | 0x3030303030303030ull;
+                const uint64_t s = (dig >> (8 * (8 - nd))) | ((uint64_t)(last ? ']' : ' ') << (8 * nd));
                 uint8_t* d = out + o;
                 if (len == 8u) {
                     __builtin_memcpy(d, &s, 8);
