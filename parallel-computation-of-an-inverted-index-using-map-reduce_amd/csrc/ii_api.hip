@@ -84,6 +84,8 @@ struct ii_ctx {
     bool pairs32 = false;   // uniq holds compact u32 pairs (k_uniq_sweep uniq32): formatted, never exported
     DBuf fbase;             // per word key: output byte of its first posting minus P[first pair]
     DBuf dhist, lbstat, ticket;  // onesweep token-sort passes: digit counts / bases, look-back entries, tile ticket
+    DBuf shist;                  // run_sort_sweep: every pass's digit counts, then bases
+    bool on_side = false;        // inside a SideScope (c->st is st2): the look-back buffers belong to the main stream
     DBuf msd;                    // packed token sort: bucket geometry, per-bucket digit counts and bases
     DBuf tbk;                    // packed token sort: bucket of every tile (u16)
     uint64_t lb_cap = 0;         // look-back entries allocated (and cleared)
@@ -390,6 +392,45 @@ static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k
 // and compacts each workgroup's range into *k2; that pass's scatter reads the
 // kept ranges back into *k, and the remaining passes run over the kept
 // records only.  *n_out receives the number of records kept.
+// The same sort without a first pass, by onesweep passes: one read of the
+// keys counts every pass's digits (k_hist_passes), then one launch per pass
+// (decoupled look-back: no per-pass histogram, table scan or scan launches).
+// The dictionary's key / index sorts of the exchange path and the owner's
+// import ran 8 x (histogram + scan + scatter) small launches before.  Main
+// stream only: the look-back entries and the tile ticket are the token sort's.
+static int run_sort_sweep(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo,
+                          int hi, int* passes) {
+    const int npass = (hi - lo + kRadixBits - 1) / kRadixBits;
+    const int bits = (hi - lo + npass - 1) / npass;
+    if (npass > kHistMaxPasses) return II_ERR_INTERNAL;
+    CK(grow(c->shist, sizeof(uint64_t) * 2 * kHistMaxPasses * kRadix));
+    uint64_t* counts = P_<uint64_t>(c->shist);
+    uint64_t* bases = counts + kHistMaxPasses * kRadix;
+    HIPCK(hipMemsetAsync(counts, 0, sizeof(uint64_t) * npass * kRadix, c->st));
+    k_hist_passes<<<(uint32_t)std::min<uint64_t>(4 * (uint64_t)c->ncu, grid_for(n)), kBlock, 0, c->st>>>(
+        *k, n, lo, hi, bits, npass, counts);
+    k_digit_bases<<<npass, kRadix, 0, c->st>>>(counts, bases);
+    HIPCK(hipGetLastError());
+    const uint64_t ntiles = (n + kSweepTile - 1) / kSweepTile;
+    for (int p = 0; p < npass; p++) {
+        const int shift = lo + p * bits, db = std::min(bits, hi - shift);
+        CK(lookback_pass(c, ntiles * kRadix));
+        if (v)
+            k_onesweep<kSweepThreads, kSweepItems, 2, true><<<(uint32_t)ntiles, kSweepThreads, 0, c->st>>>(
+                *k, *k2, n, shift, db, bases + (uint64_t)p * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket),
+                c->lb_epoch, P_<unsigned long long>(c->counters) + C_OVERFLOW, *v, *v2);
+        else
+            k_onesweep<kSweepThreads, kSweepItems><<<(uint32_t)ntiles, kSweepThreads, 0, c->st>>>(
+                *k, *k2, n, shift, db, bases + (uint64_t)p * kRadix, P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket),
+                c->lb_epoch, P_<unsigned long long>(c->counters) + C_OVERFLOW, nullptr, nullptr);
+        HIPCK(hipGetLastError());
+        std::swap(*k, *k2);
+        if (v) std::swap(*v, *v2);
+        if (passes) (*passes)++;
+    }
+    return II_OK;
+}
+
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
                     bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr,
                     bool wid = false) {
@@ -397,6 +438,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
     if (n_out) *n_out = n;
     if (hi <= lo || (n <= 1 && !remap0)) return II_OK;
     if (remap0 && v) return II_ERR_INTERNAL;
+    if (!remap0 && !c->on_side && !timed && !getenv("II_SORT_NO_SWEEP")) return run_sort_sweep(c, k, k2, v, v2, n, lo, hi, passes);
     // first pass over K1's records: one workgroup (or pair) per `group` K1b chunks
     S0Geom s0{};
     if (remap0) CK(s0_geometry(c, &s0));
@@ -452,7 +494,7 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
             k_onesweep<kSweepThreads, kSweepItems><<<(uint32_t)ntiles, kSweepThreads, 0, c->st>>>(
                 src, dst, n, shift, db, dhist + kLaterDigits * kRadix + (uint64_t)(pass - 1) * kRadix,
                 P_<uint64_t>(c->lbstat), P_<uint32_t>(c->ticket), c->lb_epoch,
-                P_<unsigned long long>(c->counters) + C_OVERFLOW);
+                P_<unsigned long long>(c->counters) + C_OVERFLOW, nullptr, nullptr);
             if (ev) {
                 HIPCK(hipEventRecord(c->ev_sc[2 * c->n_sc + 1], c->st));
                 c->sc_bytes[c->n_sc] = 16 * n;
@@ -831,7 +873,7 @@ extern "C" void ii_close(ii_ctx* c) {
                    &c->ppieces,  &c->pcnt,   &c->pout,  &c->ploff, &c->chunk_files, &c->pstop, &c->wmap,
                    &c->lexw,     &c->widl,   &c->fbase, &c->pstart_w, &c->pstop_w, &c->mstart, &c->mend,
                    &c->dhist,    &c->lbstat, &c->ticket, &c->pstart_x, &c->msd, &c->tbk, &c->moff,
-                   &c->partial2, &c->rtable2, &c->kept2, &c->drank, &c->g64};
+                   &c->partial2, &c->rtable2, &c->kept2, &c->drank, &c->g64, &c->shist};
     for (DBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (auto& e : c->ev)
@@ -1329,6 +1371,7 @@ struct SideScope {
         std::swap(c->partial, c->partial2);
         std::swap(c->rtable, c->rtable2);
         std::swap(c->kept, c->kept2);
+        c->on_side = !c->on_side;
     }
 };
 

@@ -601,16 +601,20 @@ constexpr unsigned long long kLbTimeout = 8;  // error bit (counters[C_OVERFLOW]
 // 7-bit pass over 4.8e8 records: 1 -> 5.7 ms, 2 -> 2.07, 3 -> 2.11, 4 -> 2.18,
 // 8 -> 2.50: too few and the walk falls behind, too many and the granule loads
 // themselves cost).
-template <int NT, int IT, int kLbPer = 2>
+// kVals: u32 values ride with the keys (vin -> vout), as k_radix_scatter<true>
+// (the dictionary's key / index sorts, run_sort_sweep).
+template <int NT, int IT, int kLbPer = 2, bool kVals = false>
 __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                  uint64_t n, int shift, int dbits, const uint64_t* __restrict__ dbase,
                                                  uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
-                                                 uint64_t epoch, unsigned long long* __restrict__ err) {
+                                                 uint64_t epoch, unsigned long long* __restrict__ err,
+                                                 const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout) {
     constexpr int NW = NT / 64;
     constexpr int kTileN = NT * IT;
     constexpr int kDW = kRadix / 64;
     static_assert(NT >= kRadix && NT % 64 == 0, "one digit per thread of the first kRadix threads");
     __shared__ uint64_t s_keys[kTileN];
+    __shared__ uint32_t s_vals[kVals ? kTileN : 1];
     __shared__ uint32_t s_wcnt[NW][kRadix];
     __shared__ uint32_t s_tstart[kRadix];
     __shared__ uint64_t s_run[kRadix];
@@ -632,10 +636,12 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
     const uint64_t lt = lanemask_lt();
     const uint64_t wbase = tb + (uint64_t)w * 64 * IT + l;
     uint64_t key[IT];
+    uint32_t val[kVals ? IT : 1];
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const uint64_t idx = wbase + (uint64_t)k * 64;
         key[k] = idx < n ? kin[idx] : ~0ull;
+        if (kVals) val[k] = idx < n ? vin[idx] : 0u;
     }
     // ranks inside the wave: per item, the lanes sharing a digit (ballots on
     // its bits); the lowest of them adds the group's size to the wave's digit
@@ -715,6 +721,7 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
         if (wbase + (uint64_t)k * 64 < n) {
             const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
             s_keys[s_wcnt[w][d] + rank[k]] = key[k];
+            if (kVals) s_vals[s_wcnt[w][d] + rank[k]] = val[k];
         }
     }
     // look-back: sum the earlier tiles' counts of each digit until an
@@ -780,7 +787,32 @@ __global__ __launch_bounds__(NT) void k_onesweep(const uint64_t* __restrict__ ki
             const uint64_t k = s_keys[p];
             const uint32_t d = (uint32_t)(k >> shift) & dmask;
             kout[s_run[d] + (p - s_tstart[d])] = k;
+            if (kVals) vout[s_run[d] + (p - s_tstart[d])] = s_vals[p];
         }
+    }
+}
+
+// Digit counts of every LSD pass of a sort in one read of the keys: pass p's
+// digit is the key's bits [lo + p * bits, min(lo + (p + 1) * bits, hi)), counts[p * kRadix + d]
+// (zeroed beforehand); per-workgroup LDS counters, then one global atomic per
+// non-zero counter.  (run_sort_sweep: the onesweep passes need only these.)
+constexpr int kHistMaxPasses = 8;
+__global__ __launch_bounds__(kBlock) void k_hist_passes(const uint64_t* __restrict__ keys, uint64_t n, int lo, int hi,
+                                                        int bits, int npass, uint64_t* __restrict__ counts) {
+    __shared__ uint32_t h[kHistMaxPasses][kRadix];
+    for (int i = threadIdx.x; i < kHistMaxPasses * kRadix; i += kBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = keys[i];
+        for (int p = 0; p < npass; p++) {  // (the last pass's digit may be narrower: hi - its shift bits)
+            const int sh = lo + p * bits, db = bits < hi - sh ? bits : hi - sh;
+            atomicAdd(&h[p][(uint32_t)(k >> sh) & ((1u << db) - 1u)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < npass * kRadix; i += kBlock) {
+        const uint32_t v = (&h[0][0])[i];
+        if (v) atomicAdd((unsigned long long*)&counts[i], (unsigned long long)v);
     }
 }
 

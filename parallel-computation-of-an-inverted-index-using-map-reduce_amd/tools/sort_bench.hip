@@ -326,7 +326,7 @@ int main(int argc, char** argv) {
         epoch++;
         CK(hipMemsetAsync(ticket, 0, 4));
         k_onesweep<kSweepThreads, kSweepItems><<<(unsigned)ntiles, kSweepThreads>>>(a, b, n, shift, dbits, dbase, status,
-                                                                                     ticket, epoch, err);
+                                                                                     ticket, epoch, err, nullptr, nullptr);
     });
     unsigned long long* bad;
     CK(hipMalloc(&bad, 8));
@@ -336,7 +336,8 @@ int main(int argc, char** argv) {
         const float tt = time_best([&] {
             epoch++;
             CK(hipMemsetAsync(ticket, 0, 4));
-            k_onesweep<NT, IT, PER><<<(unsigned)nt_tiles, NT>>>(a, b, n, shift, dbits, dbase, status, ticket, epoch, err);
+            k_onesweep<NT, IT, PER><<<(unsigned)nt_tiles, NT>>>(a, b, n, shift, dbits, dbase, status, ticket, epoch, err,
+                                                                 nullptr, nullptr);
         });
         printf("onesweep lookback %2d per lane %7.3f ms  %6.2f TB/s\n", PER, tt, gb / tt);
     };
