@@ -363,6 +363,21 @@ def test_logical_shards_zipf_vs_oracle():
     assert_same(shard_and_merge(text, off, 7, id_stride=stride), exp_s, "zipf G=7, ids spread to 2^27")
 
 
+def test_generic_sort_forms_vs_oracle():
+    # the owners' dictionary and id sorts run as onesweep passes (run_sort_sweep); II_SORT_NO_SWEEP=1
+    # keeps the histogram + scan + scatter passes: both forms must give the oracle's index
+    t, off = ii_ctypes.zipf_corpus(6_000_000, 120, 60_000, 17, threads=8)
+    off = off.tolist()
+    text = t.tobytes()
+    exp = oracle_index(text, off, list(range(120)))
+    assert_same(shard_and_merge(text, off, 5), exp, "zipf G=5 onesweep sorts")
+    os.environ["II_SORT_NO_SWEEP"] = "1"
+    try:
+        assert_same(shard_and_merge(text, off, 5), exp, "zipf G=5 histogram sorts")
+    finally:
+        del os.environ["II_SORT_NO_SWEEP"]
+
+
 @pytest.mark.parametrize("case,G,balanced", [("config2", 3, False), ("zipf_small", 4, True)])
 def test_export_after_reduce(case, G, balanced):
     # ii_reduce's compact token sort consumes the K1 records; an export plan / letter
