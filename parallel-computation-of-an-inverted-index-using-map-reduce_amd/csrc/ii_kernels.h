@@ -2339,9 +2339,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restr
             const bool last = p + 1 == U || (k32 ? wn[k] != 0u : wn[k] != (uint32_t)(r[k] >> 32));
             const uint64_t o = fb[k] + pb[k] + (inc - len);
             if (nd <= 7u) {
-                // digits + separator (<= 8 bytes) built in one register, then stored with at most
-                // three sized stores (unaligned global stores are native on gfx950): one byte store
-                // per digit made the pass issue-bound.
+                // digits + separator (<= 8 bytes) built in one register, then stored with two
+                // unaligned stores (native on gfx950): one byte store per digit made the pass
+                // issue-bound.
                 // The 8 decimal digits of id (< 10^7 here, leading zeros) by SWAR: two 4-digit
                 // halves, each split into 2-digit 16-bit lanes, each lane into a tens / ones byte
                 // (multiply-shift divisions exact below 10^4 and 10^2), then the leading zeros shifted
@@ -2354,16 +2354,19 @@ __global__ __launch_bounds__(kBlock, 8) void k_fmt_posts(const uint64_t* __restr
                 B = Bz | ((B - Bz * 10u) << 8);
                 const uint64_t dig = (((uint64_t)B << 32) | A) | 0x3030303030303030ull;
                 const uint64_t s = (dig >> (8 * (8 - nd))) | ((uint64_t)(last ? ']' : ' ') << (8 * nd));
+                // two stores per posting, the second ending at its last byte: they overlap for
+                // len < 8 (the same bytes twice, from one lane), so a wave whose postings all take
+                // 4..8 bytes issues exactly two dword stores (three sized stores before: dword /
+                // short / byte; 7-byte postings, rank 7's 6-digit ids, needed all three)
                 uint8_t* d = out + o;
-                if (len == 8u) {
-                    __builtin_memcpy(d, &s, 8);
-                } else {
-                    const uint32_t lo4 = (uint32_t)s;
-                    if (len & 4u) __builtin_memcpy(d, &lo4, 4);
-                    const uint64_t t = s >> (8 * (len & 4u));
-                    const uint16_t t2 = (uint16_t)t;
-                    if (len & 2u) __builtin_memcpy(d + (len & 4u), &t2, 2);
-                    if (len & 1u) d[len & 6u] = (uint8_t)(t >> (8 * (len & 2u)));
+                if (len >= 4u) {
+                    const uint32_t a = (uint32_t)s, b = (uint32_t)(s >> (8 * (len - 4u)));
+                    __builtin_memcpy(d, &a, 4);
+                    __builtin_memcpy(d + (len - 4u), &b, 4);
+                } else {  // 2 or 3 bytes (one digit + separator, or two)
+                    const uint16_t a = (uint16_t)s, b = (uint16_t)(s >> (8 * (len - 2u)));
+                    __builtin_memcpy(d, &a, 2);
+                    __builtin_memcpy(d + (len - 2u), &b, 2);
                 }
             } else {  // ids >= 10^7: one byte per digit
                 uint64_t v = id;
