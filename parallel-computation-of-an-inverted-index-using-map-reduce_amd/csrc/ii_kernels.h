@@ -2195,15 +2195,46 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restric
 }
 
 // ---------------------------------------------------------------- K5 format
+// A word's len letters at o.  <= 12 letters: from the packed key (5-bit codes,
+// first letter highest), the bytes built in two registers and stored with two
+// overlapping stores (one byte store per letter before).  Longer words: the
+// cleaned letters of the inserting occurrence in the text (main.c:105-111),
+// read one aligned 16-byte block per load (a byte load per text byte before:
+// each letter waited a load round trip, since a load after a store waits for it).
 __device__ __forceinline__ void write_word(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t key, uint64_t rep,
                                            uint32_t len, uint8_t* __restrict__ o) {
     if ((key & 0xFull) == 0) {
-        for (uint32_t i = 0; i < len; i++) o[i] = (uint8_t)('a' - 1 + ((key >> (59 - 5 * i)) & 31ull));
+        uint64_t b0 = 0, b1 = 0;  // bytes 0..7, 8..11 (past len: 0x60, never stored)
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            const uint64_t ch = 0x60ull + ((key >> (59 - 5 * i)) & 31ull);
+            if (i < 8) b0 |= ch << (8 * i);
+            else b1 |= ch << (8 * (i - 8));
+        }
+        if (len >= 8u) {
+            const uint32_t k = len - 8u;  // the last 8 bytes: [k, len) of b0 | b1 << 64
+            const uint64_t t = k ? (b0 >> (8 * k)) | (b1 << (64 - 8 * k)) : b0;
+            __builtin_memcpy(o, &b0, 8);
+            __builtin_memcpy(o + k, &t, 8);
+        } else if (len >= 4u) {
+            const uint32_t a = (uint32_t)b0, t = (uint32_t)(b0 >> (8 * (len - 4u)));
+            __builtin_memcpy(o, &a, 4);
+            __builtin_memcpy(o + (len - 4u), &t, 4);
+        } else if (len >= 2u) {
+            const uint16_t a = (uint16_t)b0, t = (uint16_t)(b0 >> (8 * (len - 2u)));
+            __builtin_memcpy(o, &a, 2);
+            __builtin_memcpy(o + (len - 2u), &t, 2);
+        } else if (len == 1u) {
+            o[0] = (uint8_t)b0;
+        }
     } else {
         uint32_t n = 0;
-        for (uint64_t g = rep; g < nbytes && n < len; g++) {
-            uint32_t lc = letter_of(text[g]);
-            if (lc < 26u) o[n++] = (uint8_t)('a' + lc);
+        for (uint64_t g = rep & ~15ull; g < nbytes && n < len; g += 16) {
+            const uint4 v = load16(text, nbytes, (int64_t)g);
+            for (uint32_t j = g < rep ? (uint32_t)(rep - g) : 0u; j < 16u && n < len; j++) {
+                const uint32_t lc = letter_of(byte_dyn(v, j));
+                if (lc < 26u) o[n++] = (uint8_t)('a' + lc);
+            }
         }
     }
 }
