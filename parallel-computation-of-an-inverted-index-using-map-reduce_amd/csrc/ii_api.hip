@@ -1654,7 +1654,7 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     CK(grow(c->fbase, sizeof(uint64_t) * (c->wid_pairs && !c->pairs32 ? c->NW : V)));
     uint64_t* fb = P_<uint64_t>(c->fbase);
     const uint32_t* fkey = dense_wid ? P_<uint32_t>(c->didx) : c->wid_pairs && !c->pairs32 ? P_<uint32_t>(c->widl) : nullptr;
-    k_fmt_words<<<grid_for(V), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
+    k_fmt_words<<<grid_for((V + kFmtWordItems - 1) / kFmtWordItems), kBlock, 0, c->st>>>(c->text, c->nbytes, P_<uint64_t>(c->lkey), P_<uint64_t>(c->lrep),
                                                   P_<uint32_t>(c->llen), ps, pe, Pp, loff, (uint32_t)V, out, fkey, fb);
     const uint32_t gfmt = (uint32_t)std::min<uint64_t>(16384, grid_for(c->U));
     if (c->pairs32) {

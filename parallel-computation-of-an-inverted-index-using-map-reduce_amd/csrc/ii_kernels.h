@@ -2249,6 +2249,7 @@ struct OpLineOff {
     __device__ void emit(uint64_t i, uint64_t ex, uint64_t) const { loff[ord[i]] = ex; }
 };
 
+constexpr int kFmtWordItems = 4;  // words per thread of k_fmt_words
 __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                       const uint64_t* __restrict__ lex_key, const uint64_t* __restrict__ lex_rep,
                                                       const uint32_t* __restrict__ lex_len,
@@ -2256,21 +2257,35 @@ __global__ __launch_bounds__(kBlock) void k_fmt_words(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ post_end, const uint64_t* __restrict__ P,
                                                       const uint64_t* __restrict__ loff, uint32_t V, uint8_t* __restrict__ out,
                                                       const uint32_t* __restrict__ widl, uint64_t* __restrict__ fbase) {
-    uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= V) return;
-    uint64_t o = loff[j];
-    uint32_t len = lex_len[j];
-    // posting p of word j starts at fbase[key(j)] + P[p] (key = wid or lexid):
-    // one gather per posting in k_fmt_posts instead of four
-    // every load before the first store: a load issued after a store waits for it too (vmcnt counts both)
-    const uint64_t ps = P[post_start[j]], pe = P[post_end[j]];
-    const uint64_t key = lex_key[j], rep = lex_rep[j];
-    const uint32_t wl = widl ? widl[j] : j;
-    fbase[wl] = o + len + 2 - ps;
-    out[o + len + 3 + (pe - ps) - 1] = '\n';
-    write_word(text, nbytes, key, rep, len, out + o);
-    out[o + len] = ':';
-    out[o + len + 1] = '[';
+    // kFmtWordItems words per thread, strided by the grid, every load of all of them issued before the
+    // first store (a load issued after a store waits for it too: vmcnt counts both)
+    const uint32_t stride = gridDim.x * kBlock;
+    const uint32_t j0 = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t o[kFmtWordItems], ps[kFmtWordItems], pe[kFmtWordItems], key[kFmtWordItems], rep[kFmtWordItems];
+    uint32_t len[kFmtWordItems], wl[kFmtWordItems];
+#pragma unroll
+    for (int q = 0; q < kFmtWordItems; q++) {
+        const uint32_t j = j0 + q * stride;
+        const bool ok = j < V;
+        o[q] = ok ? loff[j] : 0ull;
+        len[q] = ok ? lex_len[j] : 0u;
+        // posting p of word j starts at fbase[key(j)] + P[p] (key = wid or lexid):
+        // one gather per posting in k_fmt_posts instead of four
+        ps[q] = ok ? P[post_start[j]] : 0ull;
+        pe[q] = ok ? P[post_end[j]] : 0ull;
+        key[q] = ok ? lex_key[j] : 0ull;
+        rep[q] = ok ? lex_rep[j] : 0ull;
+        wl[q] = ok ? (widl ? widl[j] : j) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kFmtWordItems; q++) {
+        if (j0 + q * stride >= V) continue;
+        fbase[wl[q]] = o[q] + len[q] + 2 - ps[q];
+        out[o[q] + len[q] + 3 + (pe[q] - ps[q]) - 1] = '\n';
+        write_word(text, nbytes, key[q], rep[q], len[q], out + o[q]);
+        const uint16_t open = (uint16_t)(':' | ('[' << 8));
+        __builtin_memcpy(out + o[q] + len[q], &open, 2);
+    }
 }
 
 // uniq keys are wids or lexids, fbase is indexed the same way (k_fmt_words).
