@@ -88,7 +88,8 @@ step() {
             "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT" \
             "SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_LDS_ATOMIC" \
             "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_BUBBLE_sum" \
-            -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify $bargs ;;
+            -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify $bargs &&
+            python3 "$T/sq_summary.py" "$OUT/sq" > "$OUT/sq_summary.txt" && echo "sq ok" ;;
     listpmc)
         timeout -k 10 120 rocprofv3 -L > "$OUT/rocprofv3_L.txt" 2>&1 && echo "listed $(wc -l < "$OUT/rocprofv3_L.txt") lines" ;;
     *)
