@@ -116,6 +116,12 @@ def lib():
     return _lib
 
 
+def bytes_at(addr, n):
+    """The n bytes at addr.  (ctypes.string_at passes its size as a C int: a
+    letter text of 4.37 GB came back as its first 79 MB.)"""
+    return bytes((ctypes.c_char * n).from_address(addr)) if n else b""
+
+
 def _check(rc, what):
     if rc != II_OK:
         raise IIError(rc, what)
@@ -224,7 +230,7 @@ class Index:
         buf = ctypes.c_char_p()
         n = ctypes.c_size_t()
         _check(lib().ii_letter_text(self.h, letter, ctypes.byref(buf), ctypes.byref(n)), "ii_letter_text")
-        return ctypes.string_at(buf, n.value) if n.value else b""
+        return bytes_at(ctypes.cast(buf, ctypes.c_void_p).value, n.value)
 
     def letters(self):
         return {chr(97 + l): self.letter_text(l) for l in range(ALPHABET)}
@@ -239,7 +245,7 @@ class Index:
             buf = ctypes.c_char_p()
             n = ctypes.c_size_t()
             _check(lib().ii_partial_text(self.h, l, ctypes.byref(buf), ctypes.byref(n)), "ii_partial_text")
-            out[chr(97 + l)] = ctypes.string_at(buf, n.value) if n.value else b""
+            out[chr(97 + l)] = bytes_at(ctypes.cast(buf, ctypes.c_void_p).value, n.value)
         return out
 
     def stats(self):

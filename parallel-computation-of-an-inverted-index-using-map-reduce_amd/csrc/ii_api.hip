@@ -106,8 +106,10 @@ struct ii_ctx {
     int part_lo[II_MAX_PARTS] = {0}, part_hi[II_MAX_PARTS] = {0};  // letter range of every export part
 
     uint64_t T = 0, V = 0, U = 0, nlong = 0, out_bytes = 0;
-    int test_lb_timeout = 0;  // test knob II_TEST_LB_TIMEOUT: the look-back timeout flag raised after K3 (1) or
-                              // after the token sort (sort: K3 must skip its work); the reduce must fail
+    int test_lb_timeout = 0;  // test knob II_TEST_LB_TIMEOUT: the look-back timeout flag raised after K3 (1),
+                              // after the token sort (sort: K3 must skip its work), after a key + value sort
+                              // by onesweep passes (sweep) or after the final-order sort (order); the reduce
+                              // (or the owner's import) must fail
     uint32_t retries = 0;
     bool mapped = false, have_pairs = false, reduced = false;
     uint64_t* rec_sorted = nullptr;
@@ -244,6 +246,7 @@ static inline size_t packed_bytes(uint64_t n) { return sizeof(uint32_t) * (n + (
 // Readbacks go through the pinned words c->hbuf: a copy into pageable memory is a synchronisation of its
 // own (two in a row cost two host round trips of GPU idle time).
 constexpr size_t kHbufWords = 128, kHbufRead = 64;
+constexpr size_t kHbufLbFlag = 12;  // counters[C_OVERFLOW] read with the dictionary's and K4's readbacks
 static int read_u64(ii_ctx* c, const void* dptr, uint64_t* out, size_t n = 1) {
     if (n > kHbufWords - kHbufRead) {  // (larger tables: straight into the caller's memory)
         HIPCK(hipMemcpyAsync(out, dptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
@@ -385,6 +388,9 @@ static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k
     else sort0_inst<false, false>(c, g, k, k2, shift, dmask, table, remap, kept, shift1, shift2, dhist);
 }
 
+// test knobs: raise error bits on the device (stream-ordered)
+__global__ void k_set_bits(uint64_t* p, unsigned long long bits) { atomicOr((unsigned long long*)p, bits); }
+
 // Stable LSD radix sort of n u64 keys (optionally with u32 values) on bits
 // [lo, hi).  On return *k / *v point at the sorted arrays (buffers swap).
 // With remap0 (token sort only, no values) the first pass is k_sort0_compact:
@@ -428,17 +434,21 @@ static int run_sort_sweep(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, 
         if (v) std::swap(*v, *v2);
         if (passes) (*passes)++;
     }
+    if (c->test_lb_timeout == 3 && v) k_set_bits<<<1, 1, 0, c->st>>>(P_<uint64_t>(c->counters) + C_OVERFLOW, kLbTimeout);
     return II_OK;
 }
 
+// sweep_ok = false keeps the histogram + scan + scatter passes, which cannot time out: for sorts whose
+// values later kernels use as indices before the host can read the look-back flag (a onesweep pass that
+// flagged kLbTimeout leaves slots of its output unwritten — stale values, out-of-range indices).
 static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32_t** v2, uint64_t n, int lo, int hi,
                     bool timed, int* passes, const uint32_t* remap0 = nullptr, uint64_t* n_out = nullptr,
-                    bool wid = false) {
+                    bool wid = false, bool sweep_ok = true) {
     if (passes) *passes = 0;
     if (n_out) *n_out = n;
     if (hi <= lo || (n <= 1 && !remap0)) return II_OK;
     if (remap0 && v) return II_ERR_INTERNAL;
-    if (!remap0 && !c->on_side && !timed && !getenv("II_SORT_NO_SWEEP")) return run_sort_sweep(c, k, k2, v, v2, n, lo, hi, passes);
+    if (!remap0 && sweep_ok && !c->on_side && !timed && !getenv("II_SORT_NO_SWEEP")) return run_sort_sweep(c, k, k2, v, v2, n, lo, hi, passes);
     // first pass over K1's records: one workgroup (or pair) per `group` K1b chunks
     S0Geom s0{};
     if (remap0) CK(s0_geometry(c, &s0));
@@ -547,7 +557,6 @@ static int run_sort(ii_ctx* c, uint64_t** k, uint64_t** k2, uint32_t** v, uint32
 }
 
 // *p |= bits (one thread; the II_TEST_LB_TIMEOUT test knob)
-__global__ void k_set_bits(uint64_t* p, unsigned long long bits) { atomicOr((unsigned long long*)p, bits); }
 
 // Stable LSD radix sort of n u32 keys on bits [0, bits): *k / *k2 ping-pong,
 // on return *k holds the sorted keys (the owner's merged pairs when lexid and
@@ -841,7 +850,11 @@ extern "C" int ii_open(ii_ctx** out, int device) {
         ii_close(c);
         return II_ERR_NOMEM;
     }
-    if (const char* e = getenv("II_TEST_LB_TIMEOUT")) c->test_lb_timeout = !strcmp(e, "1") ? 1 : !strcmp(e, "sort") ? 2 : 0;
+    if (const char* e = getenv("II_TEST_LB_TIMEOUT")) c->test_lb_timeout = !strcmp(e, "1")       ? 1
+                                                                : !strcmp(e, "sort")  ? 2
+                                                                : !strcmp(e, "sweep") ? 3
+                                                                : !strcmp(e, "order") ? 4
+                                                                                      : 0;
     c->test_collide = getenv("II_TEST_COLLIDE") && !strcmp(getenv("II_TEST_COLLIDE"), "1");
     if (getenv("II_TEST_LONG_KEY_BITS")) c->test_long_bits = std::min(64, std::max(0, atoi(getenv("II_TEST_LONG_KEY_BITS"))));
     const char* s = getenv("II_TABLE_LOG2");
@@ -1437,7 +1450,11 @@ static int dict_lex(ii_ctx* c, bool wid) {
     HIPCK(hipMemsetAsync(counters + C_TIES, 0, 2 * sizeof(uint64_t), c->st));
     k_tie_mark<<<grid_for(V), kBlock, 0, c->st>>>(sk, V, P_<uint32_t>(c->tied), counters);
     uint64_t nt;
+    // the key sort may have run as onesweep passes: its look-back flag comes back with the tie count
+    // (one synchronisation), before any kernel uses its values (di) as indices
+    HIPCK(hipMemcpyAsync(c->hbuf + kHbufLbFlag, counters + C_OVERFLOW, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
     CK(read_u64(c, counters + C_TIES, &nt));
+    if (c->hbuf[kHbufLbFlag] & kLbTimeout) return II_ERR_INTERNAL;
     if (nt) {
         CK(grow(c->tpos, sizeof(uint32_t) * nt));
         CK(grow(c->rid, sizeof(uint32_t) * nt));
@@ -1465,11 +1482,12 @@ static int dict_lex(ii_ctx* c, bool wid) {
         for (uint32_t ch = kmax; ch >= 1; ch--) {
             k_tie_keys<<<grid_for(nt), kBlock, 0, c->st>>>(c->text, c->nbytes, tv, (uint32_t)nt, tdict, dslot, rep, rid,
                                                           rfirst, ch, tk);
-            CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, 64, false, nullptr));
+            CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, 64, false, nullptr, nullptr, nullptr, false, false));
         }
         k_tie_keys<<<grid_for(nt), kBlock, 0, c->st>>>(c->text, c->nbytes, tv, (uint32_t)nt, tdict, dslot, rep, rid, rfirst,
                                                       0, tk);
-        CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, std::max(1, bitlen(nt)), false, nullptr));
+        CK(run_sort(c, &tk, &tk2, &tv, &tv2, nt, 0, std::max(1, bitlen(nt)), false, nullptr, nullptr, nullptr, false,
+                    false));
         k_tie_place<<<grid_for(nt), kBlock, 0, c->st>>>(tk, tv, (uint32_t)nt, tpos, tdict, di);
         HIPCK(hipGetLastError());
     }
@@ -1638,7 +1656,9 @@ static int order_and_format(ii_ctx* c, int copy_text) {
     uint64_t* loff = P_<uint64_t>(c->loff);
     k_order_keys<<<grid_for(V), kBlock, 0, c->st>>>(P_<uint64_t>(c->dkey), ps, pe, (uint32_t)V, dbits, ok, ov,
                                                     P_<uint32_t>(c->llen), Pp, loff);
-    CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr));
+    // (histogram passes: ov indexes loff / the formatter's tables before the host reads any flag)
+    CK(run_sort(c, &ok, &ok2, &ov, &ov2, V, 0, dbits + 5, false, nullptr, nullptr, nullptr, false, false));
+    if (c->test_lb_timeout == 4) k_set_bits<<<1, 1, 0, c->st>>>(P_<uint64_t>(c->counters) + C_OVERFLOW, kLbTimeout);
     c->ord = ov;
     HIPCK(hipEventRecord(c->ev[5], c->st));
 
@@ -1671,7 +1691,12 @@ static int order_and_format(ii_ctx* c, int copy_text) {
                                       P_<uint64_t>(c->letter_off));
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[6], c->st));
+    // every sort of this reduce has run: a look-back flag raised by any of them (K3 and the dictionary
+    // check theirs earlier) fails the reduce with the letter offsets' readback
+    HIPCK(hipMemcpyAsync(c->hbuf + kHbufLbFlag, P_<uint64_t>(c->counters) + C_OVERFLOW, sizeof(uint64_t),
+                         hipMemcpyDeviceToHost, c->st));
     CK(read_u64(c, c->letter_off.p, c->h_letter_off, II_ALPHABET + 1));
+    if (c->hbuf[kHbufLbFlag] & kLbTimeout) return II_ERR_INTERNAL;
     if (copy_text) {
         c->host_text.resize(c->out_bytes + 1);
         if (c->out_bytes)

@@ -20,6 +20,10 @@
  * when the G contexts sit on G distinct devices; when fewer devices are
  * visible the contexts share them ("G logical shards") and the
  * segments move by device copies.  Output is identical for every G.
+ * Test knob II_TEST_MULTI=1: G = 1 takes the multi-context path too — one
+ * context that exports its segment, exchanges it with itself through a real
+ * one-rank RCCL communicator (ncclCommInitRank + grouped ncclSend / ncclRecv to
+ * self) and imports it: the RCCL branch runs on a one-GPU box.
  *
  * With II_PARTIAL_FILES=1 in the environment the CLI also leaves the
  * reference's partial_<letter>.txt files in the current directory
@@ -552,7 +556,8 @@ int main(int argc, char **argv) {
     multi_run run;
     memset(&run, 0, sizeof(run));
     int rc, reported = 0;
-    if (G == 1) {
+    const char *tm = getenv("II_TEST_MULTI");
+    if (G == 1 && !(tm && !strcmp(tm, "1"))) {
         rc = ii_open(&single, 0);
         if (rc == II_OK) {
             /* files in list (= ID) order: postings come out ascending (main.c:217-226) */

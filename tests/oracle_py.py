@@ -8,6 +8,11 @@ _ORACLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 _lib = None
 
 
+def _bytes_at(addr, n):
+    # (not ctypes.string_at: it passes the size as a C int, so texts past 2 GiB came back cut)
+    return bytes((ctypes.c_char * n).from_address(addr)) if n else b""
+
+
 def _load():
     global _lib
     if _lib is None:
@@ -43,7 +48,7 @@ def oracle_index(text, file_off, file_id0, threads=1):
         rc = L.ii_oracle_index(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
                                ctypes.byref(out), loff)
     assert rc == 0
-    res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
+    res = {chr(97 + l): _bytes_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
     L.ii_oracle_free(out)
     return res
 
@@ -65,6 +70,6 @@ def oracle_partials(text, file_off, file_id0, order):
     rc = L.ii_oracle_partials(tb.ctypes.data if tb.size else None, off.ctypes.data, ids.ctypes.data, len(ids),
                               od.ctypes.data if od.size else None, len(od), ctypes.byref(out), loff)
     assert rc == 0
-    res = {chr(97 + l): ctypes.string_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
+    res = {chr(97 + l): _bytes_at(out.value + loff[l], loff[l + 1] - loff[l]) for l in range(26)}
     L.ii_oracle_free(out)
     return res

@@ -85,6 +85,19 @@ def test_cli_metrics_line(G):
     assert m["wall_ms"] > 0
 
 
+@pytest.mark.parametrize("case,split", [(c, "reference") for c in CASES] + [("config2", "balanced")])
+def test_cli_rccl_one_rank_matches_reference(case, split):
+    """The CLI's RCCL branch (host/ii_index.c receive(): ncclCommInitRank from
+    one ncclGetUniqueId, one grouped ncclSend / ncclRecv round) on a one-GPU
+    box: II_TEST_MULTI=1 sends G = 1 down the multi-context path, so the one
+    context exports its letter segment, moves it to itself through a real
+    one-rank communicator and imports it (main.c:129-130 with R = 1) —
+    byte-identical to the reference's goldens."""
+    got, expected, _, r = run_cli(case, 2, 26, {"II_GPUS": "1", "II_TEST_MULTI": "1", "II_LETTER_SPLIT": split})
+    assert_same(got, expected, "%s RCCL one rank %s" % (case, split))
+    assert r.stdout.decode().count("REDUCER\n") == 26
+
+
 def test_cli_failed_owner_exits_promptly():
     """II_TEST_FAIL=merge:3 with II_GPUS=5: owner 3's import fails and the other
     owners' threads block, as behind a faulted device (round 3's post-fault

@@ -1,5 +1,5 @@
-"""GPU, world size 2 with gloo, both ranks on cuda:0: the N > 1 product path
-end to end — files sharded by the reference's size heuristic (ii_partition,
+"""GPU, world size 2 with gloo, both ranks on cuda:0 (and world size 1 over
+RCCL): the N > 1 product path end to end — files sharded by the reference's size heuristic (ii_partition,
 main.c:300-323), map + local reduce per rank, ii_dist.exchange_and_reduce
 (export -> all-to-allv -> import -> order + format), and the owners' letters
 merged — against the reference goldens; and bench.py --gpus 2 itself."""
@@ -86,6 +86,55 @@ def test_exchange_and_reduce_gloo_world2():
                         assert got[LETTERS[l]] == b"", "rank %d holds letter %s it does not own" % (r, LETTERS[l])
             for l in LETTERS:
                 assert merged[l] == expected[l], "%s balanced=%s rep %d: letter %s differs" % (case, balanced, rep, l)
+
+
+def _rank_nccl(port, cases, q):
+    """World size 1 under backend "nccl" (RCCL): ii_dist's count exchange and
+    payload all_to_all_single run as real RCCL collectives on device tensors."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ii_ctypes
+    import ii_dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    out = []
+    try:
+        assert dist.get_backend() == "nccl" and not ii_dist._host_staged(None)
+        with ii_ctypes.Index(0) as ix:
+            for case, balanced in cases:
+                text, off, ids, _ = case_arrays(case)
+                ix.map_host(text, off, ids)
+                recv_sizes, (lo, hi) = ii_dist.exchange_and_reduce(ix, len(ids), copy_text=True, balanced=balanced)
+                out.append((case, balanced, lo[0], hi[0], recv_sizes, ix.letters()))
+        q.put((out, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((out, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_and_reduce_nccl_world1():
+    """ii_dist.exchange_and_reduce over RCCL on the one-GPU box: one rank owns
+    all 26 letters (main.c:129-130 with R = 1), its segment goes through RCCL's
+    all_to_all_single to itself, and the imported index must equal the
+    reference's goldens."""
+    cases = [(c, b) for c in ["config1", "config2", "edge", "zipf_small"] for b in (False, True)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rank_nccl, args=(_free_port(), cases, q))
+    p.start()
+    out, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    assert p.exitcode == 0
+    assert len(out) == len(cases)
+    for (case, balanced), (c, b, lo, hi, recv_sizes, got) in zip(cases, out):
+        _, _, _, expected = case_arrays(case)
+        assert (c, b, lo, hi) == (case, balanced, 0, 26)
+        assert len(recv_sizes) == 1 and recv_sizes[0] > 0
+        for l in LETTERS:
+            assert got[l] == expected[l], "%s balanced=%s over RCCL: letter %s differs" % (case, balanced, l)
 
 
 def test_bench_two_ranks_gloo_strong_scaling():

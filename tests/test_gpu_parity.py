@@ -301,35 +301,39 @@ def shard_and_merge(text, off, G, id_bound=None, balanced=False, contiguous=Fals
         sb = [g * n // G for g in range(G)]
         se = [(g + 1) * n // G for g in range(G)]
     idxs = []
-    for g in range(G):
-        fids = sorted(order[sb[g]:se[g]])
-        t = bytearray()
-        o = [0]
-        for f in fids:
-            t += text[off[f]:off[f + 1]]
-            o.append(len(t))
-        ix = ii_ctypes.Index(0)
-        ix.map_host(bytes(t), o, [f * id_stride for f in fids])
-        if pre_reduce:
-            ix.reduce()
-            assert_same(ix.letters(), oracle_index(bytes(t), o, [f * id_stride for f in fids]), "shard %d alone" % g)
-        idxs.append(ix)
-    los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else (n - 1) * id_stride + 1,
-                                             balanced=balanced)
-    merged = {}
-    for g, ix in enumerate(idxs):
-        lo, hi = los[g], his[g]
-        if not balanced:
-            assert (lo, hi) == ii_ctypes.reducer_letters(g, G)
-        got = ix.letters()
-        for l in range(26):
-            ch = chr(97 + l)
-            if lo <= l < hi:
-                merged[ch] = got[ch]
-            else:
-                assert got[ch] == b"", "rank %d holds letter %s it does not own" % (g, ch)
-        ix.close()
-    return merged
+    try:
+        for g in range(G):
+            fids = sorted(order[sb[g]:se[g]])
+            t = bytearray()
+            o = [0]
+            for f in fids:
+                t += text[off[f]:off[f + 1]]
+                o.append(len(t))
+            ix = ii_ctypes.Index(0)
+            idxs.append(ix)
+            ix.map_host(bytes(t), o, [f * id_stride for f in fids])
+            if pre_reduce:
+                ix.reduce()
+                assert_same(ix.letters(), oracle_index(bytes(t), o, [f * id_stride for f in fids]),
+                            "shard %d alone" % g)
+        los, his = ii_dist.logical_shards_reduce(idxs, id_bound if id_bound is not None else (n - 1) * id_stride + 1,
+                                                 balanced=balanced)
+        merged = {}
+        for g, ix in enumerate(idxs):
+            lo, hi = los[g], his[g]
+            if not balanced:
+                assert (lo, hi) == ii_ctypes.reducer_letters(g, G)
+            got = ix.letters()
+            for l in range(26):
+                ch = chr(97 + l)
+                if lo <= l < hi:
+                    merged[ch] = got[ch]
+                else:
+                    assert got[ch] == b"", "rank %d holds letter %s it does not own" % (g, ch)
+        return merged
+    finally:
+        for ix in idxs:
+            ix.close()
 
 
 @pytest.mark.parametrize("case,G", [("config2", 2), ("config2", 3), ("zipf_small", 4), ("edge", 5), ("rand_1", 8),
@@ -609,20 +613,31 @@ def test_tiny_shapes_logical_shards(k):
     assert_same(shard_and_merge(text, off, 3), exp, "tiny %d G=3" % k)
 
 
-@pytest.mark.parametrize("where", ["1", "sort"])
+@pytest.mark.parametrize("where", ["1", "sort", "sweep", "order"])
 def test_k3_lookback_timeout_is_an_error(where):
     """K3 and the onesweep passes flag a look-back that never resolved
     (kLbTimeout) instead of hanging; the host must turn the flag into
     II_ERR_INTERNAL, not return the wrong pairs (II_TEST_LB_TIMEOUT=1 raises
     the flag after K3; =sort after the token sort, where K3 must skip its work:
-    the records are out of place and their keys may lie past the word range)."""
+    the records are out of place and their keys may lie past the word range;
+    =sweep after a key + value sort that ran as onesweep passes — the owners'
+    dictionary sort on the main stream, whose flag is read with the tie count
+    before any kernel indexes by its values; =order after the final-order sort,
+    checked with the letter offsets' readback)."""
     text, off, ids, _ = case_arrays("config2")
     os.environ["II_TEST_LB_TIMEOUT"] = where
     try:
-        with ii_ctypes.Index(0) as ix:
-            ix.map_host(text, off, ids)
+        if where != "sweep":  # (one GPU: the dictionary sorts on the side stream, by histogram passes)
+            with ii_ctypes.Index(0) as ix:
+                ix.map_host(text, off, ids)
+                with pytest.raises(ii_ctypes.IIError) as e:
+                    ix.reduce()
+                assert e.value.code == -7
+        # through the exchange: the owners' dictionary sorts run as onesweep passes on the main stream
+        # (run_sort_sweep), the owners' final order as histogram passes
+        if where in ("sweep", "order"):
             with pytest.raises(ii_ctypes.IIError) as e:
-                ix.reduce()
+                shard_and_merge(text, off, 3)
             assert e.value.code == -7
     finally:
         os.environ.pop("II_TEST_LB_TIMEOUT", None)
