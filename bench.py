@@ -684,8 +684,8 @@ def main():
             text_raw = min(raw, K1_TEXT_RAW_PER_BYTE * B_emit)
             probe = raw - text_raw
             wr = k1["write_bytes_per_launch"]
-            k1_split = {"traffic": round(2 * text_raw + probe + wr), "traffic_text": round(2 * text_raw),
-                        "traffic_probe": round(probe), "traffic_write": round(wr),
+            k1_split = {"traffic_model": round(2 * text_raw + probe + wr), "traffic_model_text": round(2 * text_raw),
+                        "traffic_model_probe": round(probe), "traffic_model_write": round(wr),
                         "probe_bytes_per_text_byte": round(probe / B_emit, 3) if B_emit else None}
         cpu = None
         if a.cpu_baseline != "none" and world == 1:
@@ -736,14 +736,19 @@ def main():
                          "bytes_per_launch": k1_survey_b, "model": "SURVEY §8d: B + 12 T",
                          "achieved_b8t": round(em_achieved, 1), "frac_b8t": round(em_achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_launch_b8t": st.emit_bytes,
-                         # calibrated PMC traffic: x2 on the streamed text only (see K1_TEXT_RAW_PER_BYTE)
-                         "traffic": k1_split["traffic"] if k1_split else None,
-                         "traffic_text": k1_split["traffic_text"] if k1_split else None,
-                         "traffic_probe": k1_split["traffic_probe"] if k1_split else None,
-                         "traffic_write": k1_split["traffic_write"] if k1_split else None,
-                         "probe_bytes_per_text_byte": k1_split["probe_bytes_per_text_byte"] if k1_split else None,
-                         "traffic_fetch_x2": round(k1["traffic_bytes_per_launch"]) if "traffic_bytes_per_launch" in k1
+                         # measured: PMC FETCH_SIZE x2 + WRITE_SIZE per launch (MI355X_MICROARCH.md's gfx950
+                         # correction) of this very build, or null
+                         "traffic": round(k1["traffic_bytes_per_launch"]) if "traffic_bytes_per_launch" in k1
                          else None,
+                         # a MODEL split of the measured counters (not measured itself): x2 on the streamed text
+                         # only, its share of raw FETCH_SIZE calibrated on the round-3 probe-free variant
+                         # (K1_TEXT_RAW_PER_BYTE, profiles/r3_k1_pmc_1GB.txt), the probes' 64-B requests unscaled
+                         "traffic_model": k1_split["traffic_model"] if k1_split else None,
+                         "traffic_model_text": k1_split["traffic_model_text"] if k1_split else None,
+                         "traffic_model_probe": k1_split["traffic_model_probe"] if k1_split else None,
+                         "traffic_model_write": k1_split["traffic_model_write"] if k1_split else None,
+                         "traffic_model_calibration": "round-3 K1b, profiles/r3_k1_pmc_1GB.txt",
+                         "probe_bytes_per_text_byte": k1_split["probe_bytes_per_text_byte"] if k1_split else None,
                          "traffic_raw": round(k1["traffic_raw_bytes_per_launch"]) if "traffic_raw_bytes_per_launch" in k1
                          else None,
                          "traffic_note": "FETCH_SIZE counts Infinity-Cache hits too (MI355X_MICROARCH.md): the 8 MB "

@@ -417,6 +417,140 @@ int ii_oracle_partials(const unsigned char *text, const uint64_t *file_off, cons
     return 0;
 }
 
+/*
+ * Streaming, letter-range form (the oracle of BASELINE configs[4] at its full
+ * 100 GB / 10^6 files, which no single in-memory call holds): the same map and
+ * reduce rules, over batches of files given in ascending id order, keeping
+ * only words whose first letter lies in [lo, hi) (main.c:114-116 buckets by
+ * it; a reducer owns a letter range, main.c:129-130).  Every batch's files are
+ * mapped by nthreads workers into private dictionaries (contiguous file runs,
+ * as ii_oracle_index_mt) and merged, letter by letter, into the stream's
+ * dictionaries — a batch's ids all exceed the earlier batches', so appending
+ * keeps every posting list ascending.  ii_oracle_stream_letter then orders and
+ * formats one letter (or_reduce_letter) and releases its dictionary.
+ */
+typedef struct {
+    or_dict dicts[OR_ALPHA];
+    int lo, hi;
+    uint32_t last_id1; /* largest id + 1 added so far */
+} or_stream;
+
+typedef struct {
+    const unsigned char *text;
+    const uint64_t *file_off;
+    const uint32_t *file_id0;
+    uint32_t f_lo, f_hi;
+    int lo, hi;
+    or_dict dicts[OR_ALPHA];
+} or_stream_job;
+
+static void or_emit_range(void *ctx, const char *w, uint32_t n, uint32_t id1) {
+    or_stream_job *j = ctx;
+    const int l = w[0] - 'a';
+    if (l >= j->lo && l < j->hi) or_dict_add(&j->dicts[l], w, n, id1);
+}
+
+static void *or_stream_map_worker(void *p) {
+    or_stream_job *j = p;
+    for (uint32_t f = j->f_lo; f < j->f_hi; f++)
+        or_tokens(j->text + j->file_off[f], j->file_off[f + 1] - j->file_off[f], j->file_id0[f] + 1, or_emit_range, j);
+    return NULL;
+}
+
+typedef struct {
+    or_stream *st;
+    or_stream_job *jobs;
+    int njobs, next;
+    pthread_mutex_t mu;
+} or_stream_merge;
+
+static void *or_stream_merge_worker(void *p) {
+    or_stream_merge *m = p;
+    for (;;) {
+        pthread_mutex_lock(&m->mu);
+        const int l = m->st->lo + m->next++;
+        pthread_mutex_unlock(&m->mu);
+        if (l >= m->st->hi) break;
+        for (int k = 0; k < m->njobs; k++) {
+            or_dict *src = &m->jobs[k].dicts[l];
+            for (uint32_t i = 0; i < src->n; i++) or_dict_merge_entry(&m->st->dicts[l], &src->e[i]);
+            free(src->e);
+            free(src->slot);
+            memset(src, 0, sizeof(*src));
+        }
+    }
+    return NULL;
+}
+
+void *ii_oracle_stream_open(int lo, int hi) {
+    if (lo < 0 || hi > OR_ALPHA || lo > hi) return NULL;
+    or_stream *st = calloc(1, sizeof(or_stream));
+    if (st) { st->lo = lo; st->hi = hi; }
+    return st;
+}
+
+/* Add a batch: file f = text[file_off[f] .. file_off[f+1]) with id file_id0[f],
+ * ids ascending and above every id added before.  Returns 0, or -1. */
+int ii_oracle_stream_add(void *h, const unsigned char *text, const uint64_t *file_off, const uint32_t *file_id0,
+                         uint32_t nfiles, int nthreads) {
+    or_stream *st = h;
+    if (!st) return -1;
+    for (uint32_t f = 0; f < nfiles; f++) {
+        if (file_id0[f] + 1 <= st->last_id1) return -1; /* IDs must ascend across batches */
+        st->last_id1 = file_id0[f] + 1;
+    }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    or_stream_job *jobs = calloc((size_t)nthreads, sizeof(or_stream_job));
+    if (!jobs) return -1;
+    const uint64_t total = nfiles ? file_off[nfiles] - file_off[0] : 0;
+    uint32_t f = 0;
+    for (int k = 0; k < nthreads; k++) {
+        jobs[k].text = text;
+        jobs[k].file_off = file_off;
+        jobs[k].file_id0 = file_id0;
+        jobs[k].lo = st->lo;
+        jobs[k].hi = st->hi;
+        jobs[k].f_lo = f;
+        const uint64_t goal = nfiles ? file_off[0] + total * (uint64_t)(k + 1) / (uint64_t)nthreads : 0;
+        while (f < nfiles && (k == nthreads - 1 || file_off[f + 1] <= goal)) f++;
+        jobs[k].f_hi = f;
+    }
+    pthread_t th[256];
+    for (int k = 0; k < nthreads; k++) pthread_create(&th[k], NULL, or_stream_map_worker, &jobs[k]);
+    for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    or_stream_merge m;
+    memset(&m, 0, sizeof(m));
+    m.st = st;
+    m.jobs = jobs;
+    m.njobs = nthreads;
+    pthread_mutex_init(&m.mu, NULL);
+    const int nm = nthreads < st->hi - st->lo ? nthreads : st->hi - st->lo;
+    for (int k = 0; k < nm; k++) pthread_create(&th[k], NULL, or_stream_merge_worker, &m);
+    for (int k = 0; k < nm; k++) pthread_join(th[k], NULL);
+    pthread_mutex_destroy(&m.mu);
+    free(jobs);
+    return 0;
+}
+
+/* Order and format letter l (lo <= l < hi): *out (free with ii_oracle_free),
+ * *len bytes, *words lines; the letter's dictionary is released. */
+int ii_oracle_stream_letter(void *h, int l, char **out, uint64_t *len, uint64_t *words) {
+    or_stream *st = h;
+    if (!st || l < st->lo || l >= st->hi) return -1;
+    *words = st->dicts[l].n;
+    *out = or_reduce_letter(&st->dicts[l], len);
+    or_dict_free(&st->dicts[l]);
+    return 0;
+}
+
+void ii_oracle_stream_close(void *h) {
+    or_stream *st = h;
+    if (!st) return;
+    for (int l = 0; l < OR_ALPHA; l++) or_dict_free(&st->dicts[l]);
+    free(st);
+}
+
 #ifdef II_ORACLE_MAIN
 /* Same CLI as the reference: <num_mappers> <num_reducers> <input_file_list>
  * (main.c:246-260); outputs a.txt..z.txt in the CWD. */

@@ -16,6 +16,10 @@ Workloads (bench.py --workload):
                  rank 0's share of BASELINE configs[4] (100 GB, 10^6 files, vocab 10^7, seed 5)
                  over 8 GPUs: the files ii_partition (main.c:300-323, M = 8) gives shard 0,
                  with their GLOBAL ids (bench.py --workload config5 --rank-share 0/8)
+  config5        BASELINE configs[4] whole (100 GB, 10^6 files, vocab 10^7, seed 5): too large
+                 for one in-memory oracle call, so the streaming letter-range oracle
+                 (ii_oracle_stream_*) runs three passes of letter ranges, each over the whole
+                 corpus generated in batches of ascending file ids (test_config5_full_exchange)
 """
 import hashlib
 import json
@@ -45,6 +49,41 @@ def share_ids(p, rank, world):
 OUT = os.path.join(HERE, "bench_hashes.json")
 
 
+# configs[4] whole: letter ranges per pass (about equal pairs each: the owners' counts of
+# test_config5_full_exchange) and files per generated batch
+C5_PASSES = [(0, 6), (6, 15), (15, 26)]
+C5_BATCH = 40_000
+
+
+def config5_stream(p, threads=8):
+    import ii_ctypes
+    from oracle_py import OracleStream
+    letters, t0 = {}, time.time()
+    corpus = None
+    for lo, hi in C5_PASSES:
+        st = OracleStream(lo, hi)
+        h_corpus = hashlib.sha256() if corpus is None else None
+        for a in range(0, p["nfiles"], C5_BATCH):
+            ids = list(range(a, min(p["nfiles"], a + C5_BATCH)))
+            text, off = ii_ctypes.zipf_shard(p["total_bytes"], p["nfiles"], p["vocab"], p["seed"], ids,
+                                             threads=threads)
+            if h_corpus is not None:
+                h_corpus.update(memoryview(text))
+            st.add(text, off, ids, threads=threads)
+            del text
+            print("  letters %s-%s: files < %d (%.0fs)" % (chr(97 + lo), chr(96 + hi), ids[-1] + 1,
+                                                           time.time() - t0), flush=True)
+        if h_corpus is not None:
+            corpus = h_corpus.hexdigest()
+        for l in range(lo, hi):
+            h = hashlib.sha256()
+            nbytes, lines = st.letter(l, h.update)
+            letters[chr(97 + l)] = {"sha256": h.hexdigest(), "bytes": nbytes, "lines": lines}
+            print("  letter %s: %d lines, %d bytes" % (chr(97 + l), lines, nbytes), flush=True)
+        st.close()
+    return letters, corpus, time.time() - t0
+
+
 def main(names):
     import ii_ctypes
     from oracle_py import oracle_index
@@ -53,6 +92,16 @@ def main(names):
         base, _, share = name.partition("/")
         p = WORKLOADS[base]
         t0 = time.time()
+        if name == "config5":
+            letters, corpus_sha, secs = config5_stream(p)
+            db["workloads"][name] = {"iigen": p, "corpus_sha256": corpus_sha, "letters": letters,
+                                     "files": p["nfiles"], "bytes": p["total_bytes"],
+                                     "out_bytes": sum(x["bytes"] for x in letters.values()),
+                                     "words": sum(x["lines"] for x in letters.values()),
+                                     "oracle_seconds": round(secs, 1), "oracle": "stream, letter passes %s" % C5_PASSES}
+            print(name, "words", db["workloads"][name]["words"], "out", db["workloads"][name]["out_bytes"], flush=True)
+            json.dump(db, open(OUT, "w"), indent=1, sort_keys=True)
+            continue
         if share:  # "share<r>of<N>": one rank's ii_partition shard, global ids
             r, n = (int(x) for x in share[len("share"):].split("of"))
             ids = share_ids(p, r, n)

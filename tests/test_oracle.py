@@ -88,3 +88,27 @@ def test_partition_order_is_size_order():
         sizes = [len(files[p]) if p in files else 0 for p in paths]
         order, sb, se = ii_ctypes.partition(sizes, 1)
         assert order == size_order(case) and (sb[0], se[0]) == (0, len(paths))
+
+
+def test_streaming_oracle_matches_whole_corpus():
+    """The streaming, letter-range oracle (configs[4]'s hashes) gives the
+    whole-corpus oracle's letters: files in 4 ascending-id batches, the
+    letters in three passes of ranges."""
+    import hashlib
+    import ii_ctypes
+    from oracle_py import OracleStream, oracle_index
+    t, off = ii_ctypes.zipf_corpus(3_000_000, 57, 40_000, 9, threads=4)
+    off = [int(x) for x in off]
+    ids = [3 * f + 1 for f in range(57)]  # ascending, not dense
+    exp = oracle_index(t, off, ids)
+    cuts = [0, 5, 23, 40, 57]
+    for lo, hi in [(0, 9), (9, 10), (10, 26)]:
+        st = OracleStream(lo, hi)
+        for a, b in zip(cuts, cuts[1:]):
+            st.add(t[off[a]:off[b]], [o - off[a] for o in off[a:b + 1]], ids[a:b], threads=3)
+        for l in range(lo, hi):
+            h = hashlib.sha256()
+            nbytes, lines = st.letter(l, h.update)
+            e = exp[chr(97 + l)]
+            assert (h.hexdigest(), nbytes, lines) == (hashlib.sha256(e).hexdigest(), len(e), e.count(b"\n"))
+        st.close()
