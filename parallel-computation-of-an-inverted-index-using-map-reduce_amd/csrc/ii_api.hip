@@ -990,6 +990,15 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     // occupancy count and the dictionary's slot compaction read every slot (2^22 of them: 32 MB for
     // the 4·10^4 big-table words of configs[2])
     if (!dense && c->big_next && c->big_next < c->big_cap && !c->big_fixed) c->big_cap = c->big_next;
+    // a context with no reduce to size it by (the CLI's only map): the big table from the input's size
+    // — about one slot per 768 bytes, 2^22 .. 2^26 slots (16 B each: keys + occurrences).  With the
+    // 2^22 of round 5 the first map of configs[4]'s rank-7 share (6.7e6 words in 12.5 GB) filled the
+    // table, and K1b ran a void attempt before the regrow: 58.6 ms of map instead of ~26.
+    if (!dense && !c->big_next && !c->big_fixed && c->text_is_input) {
+        uint64_t want = 1ull << 22;
+        while (want < (1ull << 26) && want < c->nbytes / 768) want <<= 1;
+        c->big_cap = std::max(c->big_cap, want);
+    }
     const uint64_t nch = (c->nbytes + kChunk - 1) / kChunk;
     const uint32_t wg_chunks = (uint32_t)((nch + kWG - 1) / kWG);  // K1 kernels: one wave per chunk
     c->nch_map = nch;
@@ -1075,6 +1084,10 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         if ((cnt[C_OVERFLOW] & 1) || cnt[C_INSERT] > kHotSlots / 2 + c->big_cap / 2) {
             c->big_cap *= 4;
             c->retries++;
+            // more words than the hot level and a 2^22-slot big table hold: most of them live in the
+            // big table, so the retry probes the bucket and the big home at once (DeepProbe; a context
+            // with history chose it from its last reduce already)
+            if (c->big_cap >= (1ull << 24) && c->text_is_input) c->deep_probe = true;
             continue;
         }
         if (cnt[C_OVERFLOW] & 2) {

@@ -408,15 +408,27 @@ def test_config5_shape_vs_oracle(nf):
     t, off = ii_ctypes.zipf_corpus(300_000_000, nf, 10_000_000, 5, threads=16)
     ids = list(range(nf))
     exp = oracle_index(t, off, ids, threads=16)
-    with ii_ctypes.Index(0) as ix:
-        # most words overflow the hot level: the first map probes two pairs (K1c resolves the big-table
-        # words), and the next map of the context knows it and takes DeepProbe (bucket + big home)
-        for deep in (0, 1):
-            ix.map_host(t, off.tolist(), ids)
-            ix.reduce()
-            assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7, deep probe %d" % (nf, deep))
-            st = ix.stats()
-            assert st.deep_probe == deep
+    os.environ["II_TABLE_LOG2"] = "24"  # (a big table that holds the vocabulary: no regrow)
+    try:
+        with ii_ctypes.Index(0) as ix:
+            # most words overflow the hot level: the first map probes two pairs (K1c resolves the
+            # big-table words), and the next map of the context knows it and takes DeepProbe (bucket +
+            # big home)
+            for deep in (0, 1):
+                ix.map_host(t, off.tolist(), ids)
+                ix.reduce()
+                assert_same(ix.letters(), exp, "300 MB, %d files, vocab 1e7, deep probe %d" % (nf, deep))
+                st = ix.stats()
+                assert st.deep_probe == deep and st.retries == 0
+    finally:
+        del os.environ["II_TABLE_LOG2"]
+    with ii_ctypes.Index(0) as ix2:
+        # a cold context sizes its big table by the input (2^22 slots for 300 MB): the vocabulary
+        # overflows it, the map regrows the table and its retry takes DeepProbe
+        ix2.map_host(t, off.tolist(), ids)
+        ix2.reduce()
+        assert_same(ix2.letters(), exp, "300 MB, %d files, vocab 1e7, cold context" % nf)
+        assert ix2.stats().retries >= 1 and ix2.stats().deep_probe == 1
     assert st.words == sum(v.count(b"\n") for v in exp.values()) and st.words > 3_000_000
     assert st.sort_packed == 1 and st.sort_key_bits + st.sort_id_bits - 32 <= 11
     assert st.sort_id_bits == (nf - 1).bit_length()
