@@ -1728,6 +1728,10 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)
             if (tb + tofs + (uint64_t)k * 64 == last) s_last[par] = (uint32_t)raw[k];  // (the low half is the file)
+        // the record set (small files): the next tile's loads go out before the barrier, in flight while
+        // the wave waits there (rank 7 of configs[4]: first pass 8.84 -> 8.19 ms, 214.0 -> 217.0 GB/s;
+        // the bitmap form at config3 got slower, 3.83 -> 4.18 ms, and issues them after it)
+        if (kHashD && tb + kTile < hi) load_tile(tb + kTile);
         __syncthreads();  // (s_wtot[par] and s_last[par] are rewritten two tiles later, after the next barrier)
         uint32_t wbase = 0, ttot = 0;
 #pragma unroll
@@ -1736,7 +1740,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             if (ww < w) wbase += c;
             ttot += c;
         }
-        if (tb + kTile < hi) load_tile(tb + kTile);
+        if (!kHashD && tb + kTile < hi) load_tile(tb + kTile);
 #pragma unroll
         for (int k = 0; k < kS0Items; k++) {
             if ((keep >> k) & 1u) {
