@@ -139,6 +139,7 @@ struct ii_ctx {
     int pk_F = 0, pk_L = 0;
     uint64_t n_pending = 0; // tokens K1b left to K1c
     bool deep_probe = false; // K1b's DeepProbe: most distinct words of the context's last reduce lived in the big table
+    uint32_t rec_lbits = 0;  // the last map's narrow records: slot << rec_lbits | file - the chunk's first file
     bool map_deep = false;   // the last map ran K1b with DeepProbe
     uint64_t rec_cap = 0;   // K1 record layout: kChunkCap per chunk, or 0 = dense (counted)
     uint64_t nch_map = 0;   // K1b chunks of the last map
@@ -367,10 +368,11 @@ static uint64_t s0_bytes(uint64_t n_in, uint64_t n_narrow, uint64_t n_kept) {
 template <bool kWid, bool kWideD, bool kHashD = false>
 static void sort0_inst(ii_ctx* c, const S0Geom& g, const uint64_t* k, uint64_t* k2, int shift, uint32_t dmask,
                        uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2, uint64_t* dhist) {
-    k_sort0_compact<kWid, kWideD, kHashD><<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
+    (c->rec_lbits ? k_sort0_compact<kWid, kWideD, kHashD, true> : k_sort0_compact<kWid, kWideD, kHashD, false>)
+        <<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
         k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
         (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files),
-        P_<unsigned long long>(c->totals) + 8);
+        P_<unsigned long long>(c->totals) + 8, c->rec_lbits);
 }
 static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k, uint64_t* k2, int shift,
                          uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
@@ -1057,10 +1059,11 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
         c->map_deep = c->deep_probe;
         auto* emit = nkeys == kNarrowKeys ? (c->deep_probe ? k_tok_emit<false, true> : k_tok_emit<false, false>)
                                           : (c->deep_probe ? k_tok_emit<true, true> : k_tok_emit<true, false>);
+        c->rec_lbits = rec_lbits(nslots, c->nbytes, c->nfiles);
         emit<<<wg_chunks, kBlock, 0, c->st>>>(
             c->text, c->nbytes, nch, fstart, chunk_cnt, c->rec_cap, tab, P_<uint64_t>(c->rec),
             P_<uint32_t>(c->chunk_hist), P_<uint32_t>(c->pend), P_<uint32_t>(c->pend_cnt), P_<uint32_t>(c->chunk_files),
-            P_<LongTok>(c->longs), c->long_cap / kLongShards, nkeys);
+            P_<LongTok>(c->longs), c->long_cap / kLongShards, nkeys, c->rec_lbits);
         HIPCK(hipEventRecord(c->ev_emit[1], c->st));
         k_long_totals<<<1, 64, 0, c->st>>>(counters);
         CK(run_reduce(c, OpPendCount{P_<uint32_t>(c->pend_cnt)}, nch, totals + 5));

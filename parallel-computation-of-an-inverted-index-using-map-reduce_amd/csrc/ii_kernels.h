@@ -489,9 +489,24 @@ __device__ __forceinline__ uint64_t chunk_base(const uint64_t* chunk_off, uint64
 // keep their keys in the second half (kNarrowKeys u64 entries, in miss order);
 // a chunk with more misses than that (narrow_keys, kNarrowKeys unless a test
 // lowers it with II_NARROW_KEYS) sends the rest down the general path.
+// Round 6: a chunk over several files is narrow too when their number fits the low lbits of
+// a u32 record: slot << lbits | (file - the chunk's first file), lbits = 32 - the bits of the
+// map's slots (rec_lbits; 10 at config3, 7 for configs[4]'s shares); a one-file chunk's record
+// stays its slot.  configs[4]'s rank-7
+// share (440 000 files of ~28 KB: most chunks span two or three) wrote 8-B records for nearly
+// every token before.
 constexpr uint32_t kNarrowKeys = (uint32_t)(kChunkCap / 2);
-__device__ __forceinline__ bool chunk_narrow(uint64_t cap, const uint32_t* cf, uint64_t c) {
-    return cap && cf[3 * c] == cf[3 * c + 1];
+__device__ __forceinline__ bool chunk_narrow(uint64_t cap, const uint32_t* cf, uint64_t c, uint32_t lbits) {
+    return cap && cf[3 * c + 1] - cf[3 * c] < (1u << lbits);  // (lbits = 0: one-file chunks only)
+}
+// host: the low record bits left beside a slot, or 0 (one-file narrow chunks only) for inputs of
+// large files, where few chunks span several files (config3: 2 %; the decode cost the first pass
+// 0.12 ms there and saved nothing)
+inline uint32_t rec_lbits(uint64_t nslots, uint64_t nbytes, uint64_t nfiles) {
+    if (nfiles == 0 || nbytes / nfiles >= (256u << 10)) return 0;
+    uint32_t b = 0;
+    while (b < 32 && (1ull << b) < nslots) b++;
+    return 32 - b;
 }
 // the chunk's j-th record sits at cbase (chunk_base) + ((j + rot) & wrap), (rot,
 // wrap) = (chunk_rot(c), kChunkCap - 1) in the fixed-capacity layout (u32
@@ -774,7 +789,7 @@ template <bool kSlow>
 __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text, uint64_t nbytes, uint64_t c,
                                                 const uint64_t* __restrict__ file_start, uint32_t f_lo, uint32_t f_hi,
                                                 uint64_t cbase, uint32_t wrap, uint32_t rot,
-                                                bool narrow, uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
+                                                bool narrow, uint32_t lbits, uint64_t pend_end, const uint32_t* __restrict__ pend, uint32_t n,
                                                 const Table& tab, uint64_t* __restrict__ rec, uint32_t* hist,
                                                 LongTok* __restrict__ longs, uint64_t long_per) {
     const int l = lane_id();
@@ -797,12 +812,10 @@ __device__ __forceinline__ void resolve_pending(const uint8_t* __restrict__ text
                 key = rec[cbase + (narrow ? kNarrowKeys + i : jr)];
             }
             slot = table_find(tab, key, hot_slot(key, tab.seed), pos);
-            if (narrow) {
-                reinterpret_cast<uint32_t*>(rec + cbase)[jr] = (uint32_t)slot;
-            } else {
-                const uint32_t f = f_lo == f_hi ? f_lo : file_of(file_start, f_lo, f_hi, pos);
-                rec[cbase + jr] = (slot << 32) | f;
-            }
+            const uint32_t f = f_lo == f_hi ? f_lo : file_of(file_start, f_lo, f_hi, pos);
+            if (narrow)
+                reinterpret_cast<uint32_t*>(rec + cbase)[jr] = f_lo == f_hi ? (uint32_t)slot : ((uint32_t)slot << lbits) | (f - f_lo);
+            else rec[cbase + jr] = (slot << 32) | f;
         }
         if (!kSlow) continue;
         // hashed keys: queue for the exactness check, one atomic per wave on the chunk's shard
@@ -906,14 +919,15 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
                                                uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
                                                const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
-                                               uint64_t long_per, uint32_t narrow_keys, uint64_t c, EmitLds& W) {
+                                               uint64_t long_per, uint32_t narrow_keys, uint32_t lbits, uint64_t c,
+                                               EmitLds& W) {
     const int l = lane_id();
     const uint64_t chunk_lo = c * kChunk;
     const uint64_t chunk_hi = chunk_lo + kChunk < nbytes ? chunk_lo + kChunk : nbytes;
     // the chunk's files (k_chunk_files), wave-uniform
     const uint32_t f_lo = cf[3 * c], f_hi = cf[3 * c + 1];
     const bool fsame = f_lo == f_hi;
-    const bool narrow = chunk_narrow(cap, cf, c);
+    const bool narrow = chunk_narrow(cap, cf, c, lbits);
     // a chunk over a few files (configs[4]'s small-file shares): the starts of its files after the first,
     // wave-uniform, so that a token's file is a few compares instead of a dependent load per batch
     constexpr uint32_t kFb = 3;
@@ -1004,7 +1018,7 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
             }
             const uint32_t jr = (out + q + rot) & wrap;  // this token's record in the chunk's slot
             if (resolved) {
-                if (narrow) {
+                if (narrow && fsame) {  // (wave-uniform) a one-file chunk: the slot
                     rec32[jr] = slot;
                 } else {
                     uint32_t f = f_lo;
@@ -1014,7 +1028,8 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
                     } else {
                         f = file_of(file_start, f_lo, f_hi, lo + p);
                     }
-                    rec[cbase + jr] = ((uint64_t)slot << 32) | f;
+                    if (narrow) rec32[jr] = (slot << lbits) | (f - f_lo);
+                    else rec[cbase + jr] = ((uint64_t)slot << 32) | f;
                 }
             } else if (pf) {
                 rec[cbase + (narrow ? kNarrowKeys + npf + lanes_below(mf) : jr)] = tk.key;
@@ -1034,10 +1049,10 @@ __device__ __forceinline__ void tok_emit_chunk(const uint8_t* __restrict__ text,
     //    of this wave stored: the stores are complete (vmcnt) before the loads.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    resolve_pending<false>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, pend_end, pend, npf, tab,
-                           rec, W.hist, longs, long_per);
-    resolve_pending<true>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, pend_end, pend, nps, tab,
-                          rec, W.hist, longs, long_per);
+    resolve_pending<false>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, lbits, pend_end, pend, npf,
+                           tab, rec, W.hist, longs, long_per);
+    resolve_pending<true>(text, nbytes, c, file_start, f_lo, f_hi, cbase, wrap, rot, narrow, lbits, pend_end, pend, nps,
+                          tab, rec, W.hist, longs, long_per);
     wave_sync();
     if (l < 26) chunk_hist[c * 26 + l] = W.hist[l];
     if (l == 0) {
@@ -1059,7 +1074,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
                                                      uint64_t* __restrict__ rec, uint32_t* __restrict__ chunk_hist,
                                                      uint32_t* __restrict__ pend, uint32_t* __restrict__ pend_cnt,
                                                      const uint32_t* __restrict__ cf, LongTok* __restrict__ longs,
-                                                     uint64_t long_per, uint32_t narrow_keys) {
+                                                     uint64_t long_per, uint32_t narrow_keys, uint32_t lbits) {
     __shared__ __attribute__((aligned(16))) EmitLds s_lds[kWG];
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // one chunk per wave (waves that loop over chunks, a grid of the resident workgroups: emit 11.46 -> 12.98 ms
@@ -1068,7 +1083,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_tok_emit(const uint8_t* __restric
     if (c < nch)
         tok_emit_chunk<typename std::conditional<kDeep, DeepProbe, HotProbe>::type>(
             text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf, longs, long_per,
-            kKeysArg ? narrow_keys : kNarrowKeys, c, s_lds[w]);
+            kKeysArg ? narrow_keys : kNarrowKeys, lbits, c, s_lds[w]);
 }
 
 // counters[C_HIST + l] = sum over chunks of chunk_hist[chunk][l]: the
@@ -1511,7 +1526,15 @@ constexpr int kHsRounds = 2;  // probe rounds batched over a thread's items (the
 constexpr uint32_t kHsEmpty = ~0u;
 constexpr uint32_t kHsSlotLimit = (1u << 25) - 1u;  // slots below it are probed
 constexpr uint32_t kHsFileWin = 64;                 // files past the epoch that are probed
-template <bool kWid, bool kWideD = false, bool kHashD = false>
+// A narrow chunk's u32 record as slot << 32 | file.  cfid: the chunk's first file f0, bit 31 set
+// when the chunk spans several files (record = slot << lbits | file - f0; else the slot).
+constexpr uint32_t kCfMulti = 0x80000000u;
+__device__ __forceinline__ uint64_t narrow_rec(uint32_t x, uint32_t cfid, uint32_t lbits) {
+    const uint32_t lb = (cfid & kCfMulti) ? lbits : 0u;
+    return ((uint64_t)(x >> lb) << 32) | ((cfid & ~kCfMulti) + (x & ((1u << lb) - 1u)));
+}
+// kMulti: the map wrote multi-file narrow chunks (rec_lbits != 0)
+template <bool kWid, bool kWideD = false, bool kHashD = false, bool kMulti = false>
 __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __restrict__ keys,
                                                            const uint64_t* __restrict__ voff, uint32_t nch_in,
                                                            uint32_t group, uint64_t cap, int shift, uint32_t dmask,
@@ -1520,7 +1543,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
                                                            int shift1, int shift2, uint64_t* __restrict__ dhist,
                                                            const uint32_t* __restrict__ cf,
-                                                           unsigned long long* __restrict__ narrow_recs) {
+                                                           unsigned long long* __restrict__ narrow_recs, uint32_t lbits) {
     constexpr int NT = kCBlock, NWv = kCWaves;
     constexpr int kTile = kCTile;
     constexpr uint32_t kBmWords = kDedupWords;
@@ -1529,7 +1552,7 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     __shared__ uint32_t cnt[kCntRows][kCntD];
     __shared__ uint32_t bm[kBmWords];  // the bitmap, or (kHashD) the set
     __shared__ uint32_t s_voff[kCMaxGroup + 1];  // voff[c0 + i] - voff[c0] (< group * kChunkCap)
-    __shared__ uint32_t s_cfid[kCMaxGroup];      // narrow chunk: its file id; ~0: u64 records
+    __shared__ uint32_t s_cfid[kCMaxGroup];      // narrow chunk: its first file (| kCfMulti: several); ~0: u64 records
     __shared__ uint32_t s_later[kLaterDigits][kRadix];
     __shared__ uint32_t s_wtot[2][NWv];          // per tile parity: one barrier per tile
     __shared__ uint32_t s_last[2];               // per tile parity: file of the tile's last record
@@ -1540,7 +1563,10 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     for (uint32_t i = threadIdx.x; i < kBmWords; i += NT) bm[i] = kHashD ? kHsEmpty : 0u;
     const uint64_t lo = voff[c0], hi = voff[c0 + ng];
     for (uint32_t i = threadIdx.x; i <= ng; i += NT) s_voff[i] = (uint32_t)(voff[c0 + i] - lo);
-    for (uint32_t i = threadIdx.x; i < ng; i += NT) s_cfid[i] = chunk_narrow(cap, cf, c0 + i) ? cf[3 * (c0 + i) + 2] : ~0u;
+    for (uint32_t i = threadIdx.x; i < ng; i += NT)
+        s_cfid[i] = chunk_narrow(cap, cf, c0 + i, lbits)
+                        ? cf[3 * (c0 + i) + 2] | (kMulti && cf[3 * (c0 + i) + 1] != cf[3 * (c0 + i)] ? kCfMulti : 0u)
+                        : ~0u;
     __syncthreads();
     if (narrow_recs && w == 0) {  // records of this range read as u32 (narrow chunks): the pass's honest read bytes
         uint32_t nr = 0;
@@ -1597,14 +1623,20 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
     };
     if (lo < hi) load_tile(lo);
     // the first tile's epoch: the file of the range's first record (every lane loads it)
-    uint32_t epoch = lo >= hi ? 0u : s_cfid[0] != ~0u ? s_cfid[0] : (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo];
+    uint32_t epoch = lo >= hi ? 0u
+                   : s_cfid[0] != ~0u
+                       ? (uint32_t)narrow_rec(reinterpret_cast<const uint32_t*>(keys + (uint64_t)c0 * cap)[chunk_rot(c0)],
+                                              s_cfid[0], lbits)
+                       : (uint32_t)keys[cap ? (uint64_t)c0 * cap + chunk_rot(c0) : lo];
     uint32_t par = 0;
     uint32_t ec = epoch;  // kHashD: the epoch of the set's last clear
     for (uint64_t tb = lo; tb < hi; tb += kTile, par ^= 1u) {
         uint64_t raw[kS0Items];
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)
-            raw[k] = nfid[k] == ~0u ? nraw[k] : ((nraw[k] >> (32 * ((nodd >> k) & 1u))) << 32) | nfid[k];
+            raw[k] = nfid[k] == ~0u ? nraw[k]
+                     : kMulti       ? narrow_rec((uint32_t)(nraw[k] >> (32 * ((nodd >> k) & 1u))), nfid[k], lbits)
+                                    : ((nraw[k] >> (32 * ((nodd >> k) & 1u))) << 32) | nfid[k];
         if (tb != lo && s_last[par ^ 1u] != epoch) {  // (workgroup-uniform) a new file: clear the bitmap
             epoch = s_last[par ^ 1u];
             if (!kHashD || epoch - ec >= kHsFileWin) {  // (kHashD: every 64 files)

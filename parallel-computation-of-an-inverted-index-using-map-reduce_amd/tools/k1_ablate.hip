@@ -107,7 +107,8 @@ __global__ __launch_bounds__(kBlock, 8) void k_emit_variant(const uint8_t* __res
     const uint64_t c = wave_chunk();
     if (c < nch)
         tok_emit_chunk<Probe>(text, nbytes, nch, file_start, chunk_off, cap, tab, rec, chunk_hist, pend, pend_cnt, cf,
-                              longs, long_per, narrow_keys, c, s_lds[c - (uint64_t)blockIdx.x * kWG]);
+                              longs, long_per, narrow_keys, 32u - 23u /* the 2^20 + 2^22 slots of main() */, c,
+                              s_lds[c - (uint64_t)blockIdx.x * kWG]);
 }
 
 template <class Probe>
