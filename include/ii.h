@@ -99,7 +99,7 @@ typedef struct {
     uint64_t sort_bytes;
     uint32_t sort_packed;  /* 1: the packed form (u32 records in buckets, ii_prims.h) ran */
     uint32_t sort_key_bits;  /* W: bits of the token sort's word keys */
-    uint32_t sort_id_bits;   /* F: bits of the records' shard-local file indices (packed form: W + F - 32 <= 8) */
+    uint32_t sort_id_bits;   /* F: bits of the sorted records' file fields: shard-local indices, or id0s when the first pass maps them (packed form: W + F - 32 <= 11) */
     uint32_t pair_bytes;     /* bytes per distinct pair K3 wrote: 4 (compact, formatted only) or 8 (exportable) */
     uint32_t deep_probe;     /* 1: the last map's K1b probed the whole bucket and the big-table home (large vocabulary) */
 } ii_stats;

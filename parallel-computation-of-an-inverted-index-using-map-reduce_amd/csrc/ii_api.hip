@@ -54,6 +54,9 @@ struct ii_ctx {
     // the mapped files' id0s are fid_off, fid_off + 1, ... (a caller's id range; ii_partition's size-sorted
     // shares are not): K3 adds fid_off to K1's shard-local file index instead of gathering fid[index]
     bool fid_affine = true;
+    // the packed token sort's first pass maps shard-local file indices to id0s (local_reduce):
+    // the sorted records then carry id0s, and K3 gathers nothing
+    const uint32_t* s0_fmap = nullptr;
     uint32_t fid_off = 0;
     IdDigitsTh dth{};       // K3's posting bytes by file index (pair_bytes)
     DBuf fstart, fid;
@@ -372,7 +375,7 @@ static void sort0_inst(ii_ctx* c, const S0Geom& g, const uint64_t* k, uint64_t* 
         <<<(uint32_t)g.ncol, kCBlock, 0, c->st>>>(
         k, P_<uint64_t>(c->chunk_cnt), (uint32_t)c->nch_map, (uint32_t)g.group, c->rec_cap, shift, dmask,
         (uint32_t)g.ncol, table, remap, k2, kept, shift1, shift2, dhist, P_<uint32_t>(c->chunk_files),
-        P_<unsigned long long>(c->totals) + 8, c->rec_lbits);
+        P_<unsigned long long>(c->totals) + 8, c->rec_lbits, c->s0_fmap);
 }
 static void launch_sort0(ii_ctx* c, const S0Geom& g, bool wid, const uint64_t* k, uint64_t* k2, int shift,
                          uint32_t dmask, uint64_t* table, const uint32_t* remap, uint64_t* kept, int shift1, int shift2,
@@ -607,6 +610,8 @@ static int packed_top_bits(int W, int F) {
 // more distinct pairs per file than the set holds).  II_S0_DEDUP=set|bitmap
 // (test and A/B knob) forces one.
 constexpr uint64_t kHashDedupTokens = 16384;
+// files at which the first pass maps file indices to id0s (local_reduce; a 256 KiB fmap)
+constexpr uint32_t kS0FmapFiles = 65536;
 static bool dedup_by_set(const ii_ctx* c, uint64_t n) {
     const char* e = getenv("II_S0_DEDUP");
     if (e && !strcmp(e, "set")) return true;
@@ -684,7 +689,7 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     // with 8- or 12-record tiles at 6 waves per SIMD, 3 workgroups per CU)
     if (wide) {
         auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
-                          : k_msd_scatter<NTs, ITs, kMsdMax>;
+                          : k_msd_scatter<NTs, 2 * ITs, kMsdMax>;  // (2048 digits: a 16 Ki-record tile)
         wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
     } else {
         k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
@@ -1553,7 +1558,7 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     // its lexicographic part (a sort of the V prefix keys, ~0.5 ms of small
     // launches and host round trips) runs on st2 beside the sort, queued once
     // the sort is; K3's word-id -> lexid step waits for it
-    const bool dict_side = wid;  // (same-box A/B: 394.0-394.5 GB/s with the dictionary in stream order, 395.6-396.3 beside the sort)
+    const bool dict_side = wid && !(getenv("II_DICT_SIDE") && !strcmp(getenv("II_DICT_SIDE"), "0"));  // (same-box A/B: 394.0-394.5 GB/s with the dictionary in stream order, 395.6-396.3 beside the sort)
     if (dict_side) {
         CK(dict_slots(c, true));
         HIPCK(hipEventRecord(c->ev_dict[0], c->st));
@@ -1570,15 +1575,31 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
     const int lb = std::max(1, bitlen((wid ? c->NW : V) - 1));
     uint64_t Tk = T;
     // the records carry shard-local file indices (k_chunk_files): F bits for this map's files
-    const int F = std::max(1, bitlen(c->nfiles ? c->nfiles - 1 : 0));
+    int F = std::max(1, bitlen(c->nfiles ? c->nfiles - 1 : 0));
+    // many small files with non-consecutive ids (a size-sorted ii_partition share): the first pass
+    // (its record-set form) writes id0s (F = their bits) when the packed form still holds them —
+    // K3's gather of fmap[index], in word order, missed L1 on nearly every pair (II_S0_FMAP=0|1:
+    // A/B and test knob)
+    bool s0map = false;
+    if (!c->fid_affine && c->id_bound && dedup_by_set(c, T)) {
+        const int Fg = std::max(1, bitlen(c->id_bound - 1));
+        const char* e = getenv("II_S0_FMAP");
+        if ((e ? strcmp(e, "0") != 0 : c->nfiles >= kS0FmapFiles) && packed_top_bits(lb, Fg)) {
+            F = Fg;
+            s0map = true;
+        }
+    }
     c->sort_packed = false;
     c->sort_W = lb;
     c->sort_F = F;
     const int m = packed_top_bits(lb, F);
-    if (m)
-        CK(run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
-                           &sort_passes));
-    else
+    if (m) {
+        c->s0_fmap = s0map ? P_<uint32_t>(c->fid) : nullptr;
+        const int rc = run_sort_packed(c, &r, &r2, T, 32, lb, F, m, P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid,
+                                       &sort_passes);
+        c->s0_fmap = nullptr;
+        CK(rc);
+    } else
         CK(run_sort(c, &r, &r2, nullptr, nullptr, T, 32, 32 + lb, true, &sort_passes,
                     P_<uint32_t>(wid ? c->wmap : c->remap), &Tk, wid));
     c->rec_sorted = r;
@@ -1620,7 +1641,7 @@ static int local_reduce(ii_ctx* c, bool wid, bool compact) {
         HIPCK(hipMemcpyAsync(c->hbuf, P_<uint64_t>(c->counters) + C_COLLIDE, sizeof(uint64_t), hipMemcpyDeviceToHost,
                              c->st));
     }
-    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_affine ? nullptr : P_<uint32_t>(c->fid), compact,
+    CK(run_unique(c, r, Tk, wid, c->sort_packed, c->fid_affine || s0map ? nullptr : P_<uint32_t>(c->fid), compact,
                   c->fid_affine ? c->fid_off : 0u));
     if (check) {
         c->lv_pending = false;

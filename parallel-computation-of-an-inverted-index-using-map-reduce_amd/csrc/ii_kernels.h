@@ -1543,7 +1543,8 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ kept,
                                                            int shift1, int shift2, uint64_t* __restrict__ dhist,
                                                            const uint32_t* __restrict__ cf,
-                                                           unsigned long long* __restrict__ narrow_recs, uint32_t lbits) {
+                                                           unsigned long long* __restrict__ narrow_recs, uint32_t lbits,
+                                                           const uint32_t* __restrict__ fmap) {
     constexpr int NT = kCBlock, NWv = kCWaves;
     constexpr int kTile = kCTile;
     constexpr uint32_t kBmWords = kDedupWords;
@@ -1746,20 +1747,33 @@ __global__ __launch_bounds__(kCBlock, 4) void k_sort0_compact(const uint64_t* __
             wcount += (uint32_t)__popcll(b);
             keep |= (uint32_t)ok << k;
         }
-#pragma unroll
-        for (int k = 0; k < kS0Items; k++)  // slot -> sort key, in place
-            if ((keep >> k) & 1u) {
-                const uint32_t slot = (uint32_t)(raw[k] >> 32);
-                // wid keys: only big-table words need the map (remap = wmap)
-                const uint32_t key = (kWid && slot < kHotSlots) ? slot : remap[slot];
-                raw[k] = ((uint64_t)key << 32) | (raw[k] & 0xFFFFFFFFull);
-            }
-        if (l == 0) s_wtot[par][w] = wcount;
         // the tile's last record (thread NT - 1, item kS0Items - 1; or the range's last)
         const uint64_t last = tb + kTile < hi ? tb + kTile - 1 : hi - 1;
 #pragma unroll
         for (int k = 0; k < kS0Items; k++)
             if (tb + tofs + (uint64_t)k * 64 == last) s_last[par] = (uint32_t)raw[k];  // (the low half is the file)
+        // slot -> sort key, in place; with fmap the shard-local file index -> id0 too (a tile's
+        // records come from a few neighbouring files, so these gathers hit the same lines, where
+        // K3's, in word order, missed L1 on nearly every pair; the record-set form only)
+        if (kHashD && fmap) {
+#pragma unroll
+            for (int k = 0; k < kS0Items; k++)
+                if ((keep >> k) & 1u) {
+                    const uint32_t slot = (uint32_t)(raw[k] >> 32);
+                    const uint32_t key = (kWid && slot < kHotSlots) ? slot : remap[slot];
+                    raw[k] = ((uint64_t)key << 32) | fmap[(uint32_t)raw[k]];
+                }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kS0Items; k++)
+                if ((keep >> k) & 1u) {
+                    const uint32_t slot = (uint32_t)(raw[k] >> 32);
+                    // wid keys: only big-table words need the map (remap = wmap)
+                    const uint32_t key = (kWid && slot < kHotSlots) ? slot : remap[slot];
+                    raw[k] = ((uint64_t)key << 32) | (raw[k] & 0xFFFFFFFFull);
+                }
+        }
+        if (l == 0) s_wtot[par][w] = wcount;
         // the record set (small files): the next tile's loads go out before the barrier, in flight while
         // the wave waits there (rank 7 of configs[4]: first pass 8.84 -> 8.19 ms, 214.0 -> 217.0 GB/s;
         // the bitmap form at config3 got slower, 3.83 -> 4.18 ms, and issues them after it)
@@ -1830,7 +1844,9 @@ static_assert(kUniqItems == 4, "per-item prefixes travel as 8-bit (flags) and 16
 // id0 of a record's file: the records of a map carry shard-local file indices
 // (k_chunk_files); fmap = the mapped files' id0s, or null when index == id0
 // (the file table is 0, 1, 2, ...; the owners' merged pairs carry id0s).
-// K3 (k_uniq_sweep<kPacked, kFmap>) gathers fmap[f] only in its kFmap instance.
+// K3 (k_uniq_sweep<kPacked, kFmap>) gathers fmap[f] only in its kFmap instance;
+// many small files with scattered ids (configs[4]'s rank-7 share) skip it: their
+// first pass already wrote id0s (k_sort0_compact's fmap, local_reduce).
 
 // digits of v = id0 + 1 <= 2^32 (1..10), branch-free
 __device__ __forceinline__ uint32_t id_digits(uint64_t v) {

@@ -438,9 +438,15 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin,
 // counts), reorders it in LDS and writes the u32 records low << pack_f | id in
 // runs, digit d's run at its scanned table base + pad[d] — with R >= 2^m
 // digits spread over the threads (R / NT consecutive digits each; top digits
-// up to kMsdMaxBits: the F = 19 share of configs[4] needs m = 10) and the tile
+// up to kMsdMaxBits: configs[4]'s rank-7 share needs m = 10 with 19-bit file
+// indices, m = 11 with the 20-bit id0s the first pass writes there) and the tile
 // held as the u32 records plus u16 digits, per-wave counts in u16 (a tile
-// holds < 2^16 records): 62 / 74 / 100 KiB of LDS at R = 512 / 1024 / 2048.
+// holds < 2^16 records): 62 / 74 KiB of LDS at R = 512 / 1024 (16 records a
+// thread), 148 KiB at R = 2048 with 32 a thread (local_reduce: configs[4]'s
+// rank-7 share with id0s in the records, m = 11; same-box A/B: 16 records a
+// thread, 100 KiB, 0.95 ms a step slower, non-temporal stores 0.8 ms slower —
+// the runs per digit and tile are half as long as at R = 1024,
+// profiles/r6zb_msd_scatter_2048_ab.txt).
 // (Round 4, measured and dropped: the first pass writing the records already
 // split — u32 + a u8 top digit, 5 bytes read here instead of 8 — made the
 // first pass 0.2 ms slower and this pass no faster at config3.)

@@ -7,6 +7,7 @@
 #   bench                  the default bench line (CPU baselines, io legs)
 #   quick[:ARGS]           a bench line without CPU baselines / io legs (+ARGS)
 #   prof[:ARGS]            rocprofv3 kernel statistics + trace of a quick bench (+ARGS)
+#   prof5r7[:NAME[:ENV=V,...]]  the same on configs[4]'s rank-7 share, under extra environment variables
 #   pmc                    the PMC traffic passes (profiles/pmc_traffic.py) + summary
 #   ab:VARIANTS            same-box A/B at configs[2]: base (libii.so) and libii_<v>.so
 #                          (tools/build_variant.sh / build_rev.sh); VARIANTS comma-separated
@@ -62,6 +63,15 @@ step() {
         timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
             python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify $arg \
             > "$OUT/prof.log" 2>&1 && echo "rocprof ok" ;;
+    prof5r7)
+        # rocprofv3 kernel statistics of configs[4]'s rank-7 share; arg NAME[:ENV=V,...]
+        local nm=${arg%%:*} ev=""
+        [ "$arg" != "$nm" ] && ev=${arg#*:}
+        # shellcheck disable=SC2086
+        ( [ -n "$ev" ] && export ${ev//,/ }
+          timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5r7_${nm:-base}" -o run -- \
+            python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --io-bytes 0 --no-verify --workload config5 \
+            --rank-share 7/8 > "$OUT/prof5r7_${nm:-base}.log" 2>&1 ) && echo "rocprof ok" ;;
     pmc)
         timeout -k 10 600 python3 profiles/pmc_traffic.py run "$OUT/pmc" --steps 3 --warmup 1 --no-cpu-baseline \
             --io-bytes 0 --no-verify && python3 profiles/pmc_traffic.py summarize "$OUT/pmc" > "$OUT/pmc_traffic.json" &&

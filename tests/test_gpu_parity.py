@@ -525,7 +525,7 @@ def test_wide_top_digit_vs_oracle(env):
             os.environ.pop(k, None)
 
 
-@pytest.mark.parametrize("env", [{}, {"II_PACKED_M": "10"}, {"II_SORT_KEYS": "lexid"}])
+@pytest.mark.parametrize("env", [{}, {"II_PACKED_M": "10"}, {"II_PACKED_M": "11"}, {"II_SORT_KEYS": "lexid"}])
 def test_first_pass_record_set_vs_oracle(env):
     """The first pass's record-set dedup (k_sort0_compact<.., kHashD>), the
     form small-file shares take (configs[4]'s rank 7: 3.9·10^3 tokens per
@@ -584,6 +584,48 @@ def test_global_ids_of_a_share_stay_packed():
         ix.reduce()
         assert_same(ix.letters(), exp, "global ids of a share")
         assert ix.stats().sort_packed == 1
+
+
+@pytest.mark.parametrize("fm", ["1", "0"])
+def test_first_pass_file_id_map_vs_oracle(fm):
+    """The first pass maps shard-local file indices to id0s (k_sort0_compact's
+    fmap, the record-set form; local_reduce takes it by itself from 65536
+    files, the shape of configs[4]'s rank-7 share), so the sorted records
+    carry 20-bit id0s and K3 gathers nothing.  II_S0_FMAP=1 forces it on 9000
+    small files with sparse global ids in [0, 10^6), on the same files with
+    0-100 empty files after each, on ids up to 2^31 (too many bits for the
+    packed form: the local indices stay), and on the tiny shapes; =0 keeps the
+    gather in K3.  All against the oracle."""
+    t, off = ii_ctypes.zipf_corpus(27_000_000, 9000, 1_000_000, 67, threads=8)
+    off = off.tolist()
+    rng = random.Random(67)
+    gappy = [0]
+    for o in off[1:]:
+        gappy += [gappy[-1]] * rng.randint(0, 100) + [o]
+    cases = [(t, off, sorted(rng.sample(range(1_000_000), 9000)), 20),
+             (t, gappy, sorted(rng.sample(range(1_000_000), len(gappy) - 1)), 20),
+             (t, off, sorted(rng.sample(range(1 << 31), 9000)), None)]
+    for files, ids in TINY:
+        if ids[-1] - ids[0] + 1 != len(ids):  # (consecutive ids take the affine path)
+            text = b"\n".join(files)
+            o = [0]
+            for i, f in enumerate(files):
+                o.append(o[-1] + len(f) + (1 if i + 1 < len(files) else 0))
+            cases.append((text, o, ids, None))
+    os.environ["II_S0_FMAP"] = fm
+    try:
+        for n, (text, o, ids, bits) in enumerate(cases):
+            with ii_ctypes.Index(0) as ix:
+                ix.map_host(text, o, ids)
+                ix.reduce()
+                assert_same(ix.letters(), oracle_index(text, o, ids), "II_S0_FMAP=%s case %d" % (fm, n))
+                st = ix.stats()
+                if bits:
+                    assert st.sort_packed == 1
+                    want = bits if fm == "1" else max(1, (len(o) - 2).bit_length())
+                    assert st.sort_id_bits == want, (n, st.sort_id_bits, want)
+    finally:
+        os.environ.pop("II_S0_FMAP", None)
 
 
 TINY = [
