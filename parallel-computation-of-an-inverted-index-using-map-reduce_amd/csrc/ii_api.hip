@@ -688,9 +688,16 @@ static int run_sort_packed(ii_ctx* c, uint64_t** k, uint64_t** k2, uint64_t n, i
     // (for 8-bit top digits k_msd_scatter<.., 256> measured 0.1 ms slower than k_radix_scatter<kPack>, also
     // with 8- or 12-record tiles at 6 waves per SIMD, 3 workgroups per CU)
     if (wide) {
-        auto* wk = m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
-                          : k_msd_scatter<NTs, 2 * ITs, kMsdMax>;  // (2048 digits: a 16 Ki-record tile)
-        wk<<<(uint32_t)nch, NTs, 0, c->st>>>(*k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
+        // 2048 digits: 256 threads x 32 records and u32 run bases when every position of the padded
+        // layout fits (76 KiB of LDS, two workgroups per CU), else 512 x 32 with u64 bases (148 KiB)
+        const bool run32 = n + (uint64_t)nb * kSweepTile < (1ull << 32);
+        if (m > 10 && run32)
+            k_msd_scatter<NTs / 2, 2 * ITs, kMsdMax, true><<<(uint32_t)nch, NTs / 2, 0, c->st>>>(
+                *k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
+        else
+            (m <= 9 ? k_msd_scatter<NTs, ITs, 512> : m <= 10 ? k_msd_scatter<NTs, ITs, 1024>
+                    : k_msd_scatter<NTs, 2 * ITs, kMsdMax>)<<<(uint32_t)nch, NTs, 0, c->st>>>(
+                *k2, out32, shift, m, (uint32_t)nch, table, kept, pad, F, (1u << L) - 1u);
     } else {
         k_radix_scatter<false, kScatterThreads, kScatterItems, true><<<(uint32_t)nch, kScatterThreads, 0, c->st>>>(
             *k2, (uint64_t*)nullptr, nullptr, nullptr, n, 0, shift, m, (uint32_t)nch, table, kept,

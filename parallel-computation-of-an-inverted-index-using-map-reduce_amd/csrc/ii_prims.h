@@ -441,16 +441,18 @@ __global__ __launch_bounds__(NT) void k_radix_scatter(const K* __restrict__ kin,
 // up to kMsdMaxBits: configs[4]'s rank-7 share needs m = 10 with 19-bit file
 // indices, m = 11 with the 20-bit id0s the first pass writes there) and the tile
 // held as the u32 records plus u16 digits, per-wave counts in u16 (a tile
-// holds < 2^16 records): 62 / 74 KiB of LDS at R = 512 / 1024 (16 records a
-// thread), 148 KiB at R = 2048 with 32 a thread (local_reduce: configs[4]'s
-// rank-7 share with id0s in the records, m = 11; same-box A/B: 16 records a
-// thread, 100 KiB, 0.95 ms a step slower, non-temporal stores 0.8 ms slower —
-// the runs per digit and tile are half as long as at R = 1024,
-// profiles/r6zb_msd_scatter_2048_ab.txt).
+// holds < 2^16 records): 62 / 74 KiB of LDS at R = 512 / 1024 (512 threads x
+// 16 records).  R = 2048 (local_reduce: configs[4]'s rank-7 share with id0s
+// in the records, m = 11) takes 256 threads x 32 records with u32 run bases
+// (kRun32: every position of the padded layout < 2^32), 76 KiB and two
+// workgroups per CU, else 512 x 32 with u64 bases, 148 KiB and one: 4.82
+// against 5.0 ms, the step 0.4-0.6 ms shorter (profiles/r6zf_msd_scatter_
+// two_workgroups_ab.txt; 16 records a thread at 100 KiB: 0.95 ms a step slower,
+// non-temporal stores 0.8 ms slower, profiles/r6zb_msd_scatter_2048_ab.txt).
 // (Round 4, measured and dropped: the first pass writing the records already
 // split — u32 + a u8 top digit, 5 bytes read here instead of 8 — made the
 // first pass 0.2 ms slower and this pass no faster at config3.)
-template <int NT, int IT, int R>
+template <int NT, int IT, int R, bool kRun32 = false>
 __global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__ kin, uint32_t* __restrict__ kout32,
                                                     int shift, int dbits, uint32_t nchunks,
                                                     const uint64_t* __restrict__ table,
@@ -464,7 +466,8 @@ __global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__
     __shared__ uint16_t s_dig[kTileN];
     __shared__ uint16_t s_wcnt[NW][R];
     __shared__ uint16_t s_tstart[R];
-    __shared__ uint64_t s_run[R];
+    using RunT = typename std::conditional<kRun32, uint32_t, uint64_t>::type;  // kRun32: the launcher checked
+    __shared__ RunT s_run[R];                                                    // every position < 2^32
     __shared__ uint32_t s_scan[NW];
     const int w = wave_id(), l = lane_id(), t = threadIdx.x;
     const uint32_t ndig = 1u << dbits, dmask = ndig - 1u;
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__
     const uint64_t lo = kept[kMaxChunks + blockIdx.x], hi = lo + kept[blockIdx.x];
 #pragma unroll
     for (int i = 0; i < DPT; i++)
-        if (d0 + i < ndig) s_run[d0 + i] = table[(uint64_t)(d0 + i) * nchunks + blockIdx.x] + pad[d0 + i];
+        if (d0 + i < ndig) s_run[d0 + i] = (RunT)(table[(uint64_t)(d0 + i) * nchunks + blockIdx.x] + pad[d0 + i]);
     const uint64_t lt = lanemask_lt();
     uint32_t nrec[IT], ndg[IT];
     auto load_tile = [&](uint64_t tb) {
@@ -573,7 +576,7 @@ __global__ __launch_bounds__(NT) void k_msd_scatter(const uint64_t* __restrict__
             const uint32_t p = j * NT + t;
             if (p < all) {
                 const uint32_t d = s_dig[p];
-                kout32[s_run[d] + (p - s_tstart[d])] = s_keys[p];
+                kout32[(uint64_t)s_run[d] + (p - s_tstart[d])] = s_keys[p];
             }
         }
         __syncthreads();
