@@ -628,6 +628,28 @@ def test_first_pass_file_id_map_vs_oracle(fm):
         os.environ.pop("II_S0_FMAP", None)
 
 
+def test_dictionary_in_stream_order_vs_oracle():
+    """II_DICT_SIDE=0: the dictionary's lexicographic part in stream order
+    instead of beside the token sort (its side-stream placement is what every
+    other test runs) — the reference's golden cases and a Zipf corpus."""
+    os.environ["II_DICT_SIDE"] = "0"
+    try:
+        with ii_ctypes.Index(0) as ix:
+            for case in CASES:
+                text, off, ids, expected = case_arrays(case)
+                ix.map_host(text, off, ids)
+                ix.reduce()
+                assert_same(ix.letters(), expected, "II_DICT_SIDE=0 " + case)
+            t, off = ii_ctypes.zipf_corpus(20_000_000, 300, 1_000_000, 71, threads=8)
+            off = off.tolist()
+            ids = list(range(len(off) - 1))
+            ix.map_host(t, off, ids)
+            ix.reduce()
+            assert_same(ix.letters(), oracle_index(t, off, ids), "II_DICT_SIDE=0 zipf")
+    finally:
+        os.environ.pop("II_DICT_SIDE", None)
+
+
 TINY = [
     ([b"a"], [0]),
     ([b"a b"], [4]),
