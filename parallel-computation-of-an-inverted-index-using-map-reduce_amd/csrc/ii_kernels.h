@@ -19,7 +19,10 @@
 namespace ii {
 
 // ---------------------------------------------------------------- constants
-constexpr uint64_t kChunk = 16384;  // bytes of text per K1 chunk (one wave each, see "K1 chunks")
+// bytes of text per K1 chunk (one wave each, see "K1 chunks"); 32 KiB against 16: K1b 11.68-11.74 ->
+// 11.61-11.63 ms at config3 (half the chunks' fixed costs: file bounds, the K1c tail, the histogram
+// write), configs[4]'s rank 7 unchanged; 8 KiB: 12.1 ms (profiles/r6zp_chunk_size_ab.txt)
+constexpr uint64_t kChunk = 32768;
 constexpr int kMaxWord = 299;      // MAX_WORD - 1 letters (main.c:7, 105)
 constexpr int kMaxProbe = 1 << 12;  // big-table probe bound (load <= 1/2 enforced by the host): past it, C_OVERFLOW
 
