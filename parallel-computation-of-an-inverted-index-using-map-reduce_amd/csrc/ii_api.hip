@@ -1048,8 +1048,12 @@ static int map_core(ii_ctx* c, uint64_t hist_out[II_ALPHABET], bool dense = fals
     CK(grow(c->chunk_files, sizeof(uint32_t) * 3 * nch));
     k_chunk_files<<<grid_for(nch), kBlock, 0, c->st>>>(fstart, c->nfiles, c->nbytes, kChunk, nch,
                                                       P_<uint32_t>(c->chunk_files));
-    const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;  // the long queue grows on overflow
-    if (c->long_cap < std::max<uint64_t>(1 << 16, t_est / 64)) c->long_cap = std::max<uint64_t>(1 << 16, t_est / 64);
+    // the long queue grows on overflow (a retry of the map); at least one chunk of nothing but long
+    // tokens (13 letters + a separator each) per queue shard, so that inputs of up to kLongShards
+    // chunks never retry for it
+    const uint64_t t_est = c->rec_cap ? c->nbytes / 4 : c->T;
+    const uint64_t lmin = std::max<uint64_t>((uint64_t)kLongShards * (kChunk / 14 + 1), t_est / 64);
+    if (c->long_cap < lmin) c->long_cap = lmin;
 
     // K1b, its counts, the exactness check of hashed keys, the token count scan
     // and the letter histogram are all queued before the host looks: one host
